@@ -1,0 +1,106 @@
+/* smallz4_amd.h -- C ABI of the MI355X (gfx950) LZ4 optimal-parse compressor.
+ *
+ * Drop-in boundary for the reference's compression entry point
+ *   smallz4::lz4(GET_BYTES, SEND_BYTES, maxChainLength, dictionary,
+ *                useLegacyFormat, userPtr)          reference smallz4.h:47-64
+ * Everything here is plain C: pointers, sizes, integer status codes.  The C++
+ * mirror of the reference class (include/smallz4_amd.hpp) and the Python
+ * package (smallz4_amd/) are thin layers over these symbols.
+ *
+ * Compression levels are the reference's maxChainLength (smallz4.cpp:175-239):
+ *   0 stored, 1..3 greedy, 4..6 lazy + optimal parse, 7..65534 optimal parse
+ *   with a chain limit, 65535 ("-9") unlimited optimal parse.
+ * Output is byte-identical to the reference at the same level.
+ */
+#ifndef SMALLZ4_AMD_H
+#define SMALLZ4_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define SZ4_OK              0
+#define SZ4_E_ARG          -1  /* bad argument                                  */
+#define SZ4_E_DEVICE       -2  /* HIP runtime error                             */
+#define SZ4_E_CAPACITY     -3  /* output buffer too small                       */
+#define SZ4_E_NOMEM        -4  /* device/host allocation failed                 */
+#define SZ4_E_UNSUPPORTED  -5  /* combination not implemented on the device     */
+
+/* frame header written by sz4_compress_blocks_device */
+#define SZ4_HEADER_SMALLZ4     0  /* exactly smallz4's header: 04 22 4D 18 40 70 DF  */
+#define SZ4_HEADER_INDEPENDENT 1  /* LZ4 frame flagged block-independent, BD sized   */
+#define SZ4_HEADER_NONE        2  /* no header and no end mark: bare blocks          */
+
+typedef struct sz4_ctx sz4_ctx;
+
+/* Version of the reference interface mirrored (smallz4.h:67-70). */
+const char* sz4_version(void);
+
+/* Create a compression context bound to HIP device `device`.  Scratch space is
+ * allocated lazily and grown on demand; `reserve_bytes` pre-sizes it for that
+ * much input (0 = on first use). */
+int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes);
+void sz4_destroy(sz4_ctx* ctx);
+
+/* Worst-case frame size for n input bytes cut into blocks of block_size. */
+uint64_t sz4_bound(uint64_t n, uint32_t block_size);
+
+/* Compress n bytes already resident in device memory as independent blocks of
+ * block_size bytes (last block shorter).  Each block's bytes in the output
+ * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
+ * block compressed on its own (reference smallz4.h:476-813 with one block).
+ *
+ *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
+ *   block_size    1 .. 4 MiB
+ *   max_chain     reference maxChainLength (0..65535)
+ *   header        SZ4_HEADER_*
+ *   out_size      host pointer, receives the frame size
+ *   stream        hipStream_t (NULL = default stream); the call returns after
+ *                 the stream has finished (out_size needs the result)
+ */
+int sz4_compress_blocks_device(sz4_ctx* ctx, const void* d_in, uint64_t n, uint32_t block_size,
+                               uint32_t max_chain, int header, void* d_out, uint64_t out_cap,
+                               uint64_t* out_size, void* stream);
+
+/* Per-block result sizes of the last sz4_compress_blocks_device call
+ * (4-byte word included), copied to host array sizes[0..nblocks).  Returns the
+ * number of blocks, or a negative status. */
+int64_t sz4_last_block_sizes(sz4_ctx* ctx, uint32_t* sizes, uint64_t max_blocks);
+
+/* Whole-stream compression with the exact semantics of
+ * smallz4::lz4(getBytes, sendBytes, maxChainLength, dictionary, useLegacyFormat)
+ * (reference smallz4.h:47-64): 4 MiB dependent blocks (8 MiB independent
+ * blocks in legacy format), optional dictionary, identical output bytes.
+ * Host buffers; the device does all compression work. */
+int sz4_lz4(sz4_ctx* ctx, const void* in, uint64_t n, uint32_t max_chain, const void* dict,
+            uint64_t dict_len, int legacy, void* out, uint64_t out_cap, uint64_t* out_size);
+
+/* Worst-case size of sz4_lz4's output. */
+uint64_t sz4_lz4_bound(uint64_t n, int legacy);
+
+/* Device time (milliseconds) of each pipeline stage of the last call, measured
+ * with HIP events on the call's stream.  stage_ms[0..n) receives
+ * {runs, sort, find, parse, assemble}; returns the number of stages. */
+int sz4_last_stage_ms(sz4_ctx* ctx, float* stage_ms, int n);
+
+/* Enable (1) or disable (0) per-stage event timing (default off). */
+void sz4_set_timing(sz4_ctx* ctx, int on);
+
+/* Diagnostics: stop the pipeline after stage `stop_after` (0 = run everything,
+ * 3 = after the match search, 4 = after the parse) on subsequent calls, and copy
+ * the per-position match arrays of the last call (length u32, distance u16, one
+ * entry per input byte) to host memory.  Used by the intermediate parity tests. */
+void sz4_debug_stop_after(sz4_ctx* ctx, int stop_after);
+int sz4_debug_matches(sz4_ctx* ctx, uint32_t* len, uint16_t* dist, uint64_t n);
+
+/* Last error message of the context ("" if none). */
+const char* sz4_last_error(sz4_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SMALLZ4_AMD_H */

@@ -1,0 +1,160 @@
+"""smallz4_amd -- LZ4 optimal-parse compression (smallz4 semantics) on MI355X.
+
+Python mirror of the reference's public interface (reference smallz4.h:38-80):
+
+    smallz4_amd.lz4(data, max_chain_length=65535, dictionary=b"", use_legacy_format=False)
+        == bytes the reference's smallz4::lz4(...) emits for `data`
+    smallz4_amd.ShortChainsGreedy / ShortChainsLazy / get_version()
+
+plus the data-parallel entry point the GPU is built for:
+
+    Compressor().compress_blocks(data, block_size=65536, max_chain_length=65535)
+        -> frame whose every block equals smallz4's output for that block alone
+
+All compression runs in the HIP library smallz4_amd/lib/libsmallz4_amd.so; there
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import _native
+
+ShortChainsGreedy = 3   # smallz4.h:77
+ShortChainsLazy = 6     # smallz4.h:79
+MaxChainLength = 65535  # smallz4.h:115 ("-9")
+
+HEADERS = {"smallz4": _native.SZ4_HEADER_SMALLZ4, "independent": _native.SZ4_HEADER_INDEPENDENT,
+           "none": _native.SZ4_HEADER_NONE}
+
+
+def get_version() -> str:
+    return _native.lib().sz4_version().decode()
+
+
+def level_to_chain(level: int) -> int:
+    """CLI level -0..-9 -> maxChainLength (smallz4.cpp:175, 232-239)."""
+    if not 0 <= level <= 9:
+        raise ValueError("level must be 0..9")
+    return 65535 if level == 9 else level
+
+
+class Compressor:
+    """A device context (HBM scratch stays allocated between calls)."""
+
+    def __init__(self, device: int = 0, reserve_bytes: int = 0):
+        self._lib = _native.lib()
+        h = ctypes.c_void_p()
+        rc = self._lib.sz4_create(ctypes.byref(h), device, reserve_bytes)
+        if rc != _native.SZ4_OK:
+            raise _native.NativeError(f"sz4_create failed ({rc}): no usable HIP device {device}")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sz4_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int, what: str):
+        if rc != _native.SZ4_OK:
+            msg = self._lib.sz4_last_error(self._h).decode()
+            raise _native.NativeError(f"{what} failed ({rc}): {msg}")
+
+    # -- reference entry point ------------------------------------------------------------------
+    def lz4(self, data: bytes, max_chain_length: int = MaxChainLength, dictionary: bytes = b"",
+            use_legacy_format: bool = False) -> bytes:
+        """Byte-identical to smallz4::lz4 (smallz4.h:47-64) on the same input."""
+        data = bytes(data)
+        cap = self._lib.sz4_lz4_bound(len(data), int(use_legacy_format))
+        out = ctypes.create_string_buffer(cap)
+        size = ctypes.c_uint64()
+        dic = bytes(dictionary)
+        rc = self._lib.sz4_lz4(self._h, data, len(data), int(max_chain_length), dic if dic else None, len(dic),
+                               int(use_legacy_format), out, cap, ctypes.byref(size))
+        self._check(rc, "sz4_lz4")
+        return out.raw[:size.value]
+
+    # -- data-parallel entry point --------------------------------------------------------------
+    def compress_blocks_device(self, d_in: int, n: int, d_out: int, out_cap: int, block_size: int = 65536,
+                               max_chain_length: int = MaxChainLength, header: str = "smallz4",
+                               stream: int = 0) -> int:
+        """Device pointers in, frame size out (see sz4_compress_blocks_device)."""
+        size = ctypes.c_uint64()
+        rc = self._lib.sz4_compress_blocks_device(self._h, ctypes.c_void_p(d_in), n, block_size, int(max_chain_length),
+                                                  HEADERS[header], ctypes.c_void_p(d_out), out_cap,
+                                                  ctypes.byref(size), ctypes.c_void_p(stream))
+        self._check(rc, "sz4_compress_blocks_device")
+        return size.value
+
+    def compress_blocks(self, data, block_size: int = 65536, max_chain_length: int = MaxChainLength,
+                        header: str = "smallz4") -> bytes:
+        """Host bytes (or a uint8 torch tensor on the GPU) in, frame bytes out."""
+        import torch
+        if isinstance(data, torch.Tensor):
+            t = data.contiguous().view(torch.uint8).reshape(-1)
+            if not t.is_cuda:
+                t = t.cuda(self.device)
+        else:
+            raw = bytes(data)
+            t = torch.frombuffer(bytearray(raw), dtype=torch.uint8) if raw else torch.empty(0, dtype=torch.uint8)
+            t = t.cuda(self.device)
+        n = t.numel()
+        cap = self._lib.sz4_bound(n, block_size)
+        out = torch.empty(max(cap, 16), dtype=torch.uint8, device=t.device)
+        stream = torch.cuda.current_stream(t.device).cuda_stream
+        size = self.compress_blocks_device(t.data_ptr() if n else out.data_ptr(), n, out.data_ptr(), cap,
+                                           block_size, max_chain_length, header, stream)
+        return out[:size].cpu().numpy().tobytes()
+
+    def last_block_sizes(self, nblocks: int) -> list[int]:
+        arr = (ctypes.c_uint32 * max(nblocks, 1))()
+        k = self._lib.sz4_last_block_sizes(self._h, arr, nblocks)
+        if k < 0:
+            raise _native.NativeError("sz4_last_block_sizes failed")
+        return list(arr[:k])
+
+    def debug_stop_after(self, stage: int):
+        self._lib.sz4_debug_stop_after(self._h, int(stage))
+
+    def debug_matches(self, n: int):
+        import numpy as np
+        ln = np.zeros(n, dtype=np.uint32)
+        ds = np.zeros(n, dtype=np.uint16)
+        self._check(self._lib.sz4_debug_matches(self._h, ln.ctypes.data, ds.ctypes.data, n), "sz4_debug_matches")
+        return ln, ds
+
+    def set_timing(self, on: bool):
+        self._lib.sz4_set_timing(self._h, int(on))
+
+    def last_stage_ms(self) -> dict:
+        arr = (ctypes.c_float * 5)()
+        self._lib.sz4_last_stage_ms(self._h, arr, 5)
+        return dict(zip(["runs", "sort", "find", "parse", "assemble"], list(arr)))
+
+
+_default = None
+
+
+def _ctx() -> Compressor:
+    global _default
+    if _default is None:
+        _default = Compressor()
+    return _default
+
+
+def lz4(data: bytes, max_chain_length: int = MaxChainLength, dictionary: bytes = b"",
+        use_legacy_format: bool = False) -> bytes:
+    """smallz4::lz4 (smallz4.h:47-64) on the GPU."""
+    return _ctx().lz4(data, max_chain_length, dictionary, use_legacy_format)
+
+
+def compress_blocks(data, block_size: int = 65536, max_chain_length: int = MaxChainLength,
+                    header: str = "smallz4") -> bytes:
+    return _ctx().compress_blocks(data, block_size, max_chain_length, header)

@@ -1,0 +1,77 @@
+// sz4_internal.h -- descriptors shared by the host driver (sz4_host.cpp) and the
+// gfx950 kernels (sz4_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+namespace sz4 {
+
+// constants of the reference format (smallz4.h:92-131)
+constexpr int kMinMatch = 4;             // MinMatch
+constexpr int kTailNoMatch = 12;         // BlockEndNoMatch
+constexpr int kTailLiterals = 5;         // BlockEndLiterals
+constexpr uint32_t kWindow = 65535;      // MaxDistance
+constexpr uint32_t kSameLetter = 19 + 255 * 256;  // MaxSameLetter
+constexpr int kGreedyMax = 3;            // ShortChainsGreedy
+constexpr int kLazyMax = 6;              // ShortChainsLazy
+constexpr uint32_t kHashMul = 48271;     // getHash32 multiplier
+constexpr int kHashBits = 20;
+constexpr uint64_t kNone = ~0ull;
+
+// one LZ4 block (all positions absolute byte offsets in the staged input)
+struct Block {
+  uint64_t start, end;     // [start, end)
+  uint64_t low;            // lowest position a match may reference (reference dataZero)
+  uint64_t cut;            // start-12 when the block re-inserts the previous tail (lookback), else kNone
+  uint64_t tokOff;         // first Token slot of this block (capacity (end-start)/2 + 4)
+  uint32_t prev;           // index of the previous block of the same stream, or kNoBlock
+  uint32_t flags;          // kBlk* below
+};
+constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+constexpr uint32_t kBlkLegacy = 1;         // always emitted compressed (legacy frame)
+
+// targets [s0, s1) of one block, searched against the window [w0, s1)
+struct Segment {
+  uint64_t w0, s0, s1;
+  uint64_t elemOff;        // offset (elements) of this segment's sort scratch
+  uint64_t rankOff;        // offset (u32) of this segment's rank array (s1 - s0 entries)
+  uint32_t block;
+  uint32_t pad;
+};
+
+// positions [lo, hi) are skipped by the reference's same-letter shortcut
+// (smallz4.h:631-643): not inserted into the chains and given (dist 1, La - (p - a))
+struct Interval {
+  uint64_t lo, hi;
+  uint64_t a;              // the position whose distance-1 match starts the shortcut
+  uint64_t La;             // its match length
+};
+// block b owns iv[b * kMaxIv .. b * kMaxIv + ivCount[b])
+constexpr uint32_t kMaxIv = 136;  // > 8 MiB / 65300
+
+// one LZ4 sequence: literal run [litFrom, litFrom+lits) (block-relative) then a match
+struct Token {
+  uint32_t litFrom, lits, mlen, dist;  // dist: low 16 bits; kTokLast marks the final literals-only token
+};
+constexpr uint32_t kTokLast = 0x80000000u;
+
+// kernels (sz4_kernels.hip)
+uint32_t find_lds_bytes();
+void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount,
+                 hipStream_t s);
+void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
+                 const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
+                 uint32_t* rank, hipStream_t s);
+void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
+                 const Interval* iv, const uint32_t* ivCount, const uint2* elem, const uint32_t* rank,
+                 uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
+                 bool ldsWindow, hipStream_t s);
+void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const Interval* iv,
+                  const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
+                  uint64_t matchBase, uint32_t* cost, int* status, hipStream_t s);
+void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
+                 const uint16_t* mdist, uint64_t matchBase, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
+                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s);
+
+}  // namespace sz4

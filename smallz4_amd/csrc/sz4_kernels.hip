@@ -1,0 +1,1036 @@
+// sz4_kernels.hip -- gfx950 kernels of the LZ4 optimal-parse compressor.
+//
+// Pipeline per batch of blocks (all data resident in HBM):
+//   k_runs      same-letter runs  -> shortcut intervals     (smallz4.h:631-643)
+//   k_sort      per segment: positions sorted by (4-byte key, position); replaces
+//               the previousHash/previousExact chains        (smallz4.h:645-720)
+//   k_find      per position: longest match over the sorted candidate group,
+//               64 candidates per wavefront step             (smallz4.h:173-255)
+//   k_parse     per block, one wavefront: greedy/lazy skip scan, backward
+//               optimal parse, token emission                (smallz4.h:376-472, 259-371, 726-744)
+//   k_scan / k_assemble   block offsets + frame concatenation (smallz4.h:762-813)
+//
+// Integer/byte work only: no MFMA.  The reference semantics each kernel must
+// reproduce are restated in DESIGN.md section 3.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sz4_internal.h"
+
+namespace sz4 {
+
+// ------------------------------------------------------------------------------------------------
+// small helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ref_hash(uint32_t four)
+{
+  return ((four * kHashMul) >> (32 - kHashBits)) & ((1u << kHashBits) - 1);
+}
+
+// four bytes at any offset of a buffer whose allocation is padded by >= 8 bytes and 4-aligned
+__device__ __forceinline__ uint32_t gload4(const uint8_t* base, uint64_t off)
+{
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
+  const uint32_t lo = w[0], hi = w[1];
+  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
+}
+
+__device__ __forceinline__ uint32_t lload4(const uint32_t* w, uint32_t off)
+{
+  const uint32_t lo = w[off >> 2], hi = w[(off >> 2) + 1];
+  return __builtin_amdgcn_alignbyte(hi, lo, off & 3);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
+{
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t o = __shfl_xor(v, m, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint32_t o = __shfl_xor(v, m, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// value of a lane chosen by a wave-uniform index (v_readlane: no LDS round trip)
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
+{
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+// DPP row (16-lane) permutations
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp(uint32_t v)
+{
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, 0xF, 0xF, false);
+}
+constexpr int kQuadSwap1 = 0xB1;      // quad_perm [1,0,3,2]
+constexpr int kQuadSwap2 = 0x4E;      // quad_perm [2,3,0,1]
+constexpr int kRowHalfMirror = 0x141;
+constexpr int kRowMirror = 0x140;
+constexpr int kRowShr = 0x110;        // + n
+
+// every lane receives the min / max of its 16-lane row
+__device__ __forceinline__ uint32_t row_min(uint32_t v)
+{
+  v = min(v, dpp<kQuadSwap1>(v));
+  v = min(v, dpp<kQuadSwap2>(v));
+  v = min(v, dpp<kRowHalfMirror>(v));
+  v = min(v, dpp<kRowMirror>(v));
+  return v;
+}
+__device__ __forceinline__ uint32_t row_max(uint32_t v)
+{
+  v = max(v, dpp<kQuadSwap1>(v));
+  v = max(v, dpp<kQuadSwap2>(v));
+  v = max(v, dpp<kRowHalfMirror>(v));
+  v = max(v, dpp<kRowMirror>(v));
+  return v;
+}
+// inclusive max-scan inside each 16-lane row (lanes below the row start contribute 0)
+__device__ __forceinline__ uint32_t row_scan_max(uint32_t v)
+{
+  v = max(v, dpp<kRowShr + 1>(v));
+  v = max(v, dpp<kRowShr + 2>(v));
+  v = max(v, dpp<kRowShr + 4>(v));
+  v = max(v, dpp<kRowShr + 8>(v));
+  return v;
+}
+// wave-wide min, result uniform
+__device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
+{
+  v = row_min(v);
+  const uint32_t a = rdlane(v, 0), b = rdlane(v, 16), c = rdlane(v, 32), d = rdlane(v, 48);
+  return min(min(a, b), min(c, d));
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v)
+{
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += o;
+  }
+  return v;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v)
+{
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d && o > v) v = o;
+  }
+  return v;
+}
+
+// load that bypasses the vector L1 (sc1): for data this wavefront itself rewrote earlier in the
+// same kernel -- a plain load may hit the stale L1 line
+__device__ __forceinline__ uint32_t ld_fresh(const uint32_t* p)
+{
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// is position q inside one of `cnt` intervals of list `iv`
+__device__ __forceinline__ bool in_iv(const Interval* iv, uint32_t cnt, uint64_t q)
+{
+  for (uint32_t k = 0; k < cnt; k++)
+    if (q >= iv[k].lo && q < iv[k].hi) return true;
+  return false;
+}
+
+// ================================================================================================
+// k_runs: one workgroup per block.  A run of one byte value longer than ~65300 bytes is where the
+// reference's same-letter shortcut (smallz4.h:631-643) stops inserting positions.  For levels that
+// search every position (maxChain > 6) the shortcut is fully determined by the run:
+//   a  = first searched position of the run whose predecessor is in the run
+//        (run start + 1, or the block start when the run began in the previous block),
+//   La = min(run end, block end - 5) - a         (its distance-1 match, capped by the block),
+//   skipped positions = [a + 1, a + La - MaxSameLetter]  when La > MaxSameLetter.
+// ================================================================================================
+__global__ __launch_bounds__(256) void k_runs(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                              Interval* __restrict__ ivOut, uint32_t* __restrict__ ivCount)
+{
+  const Block B = blocks[blockIdx.x];
+  const uint32_t tid = threadIdx.x;
+  Interval* iv = ivOut + (uint64_t)blockIdx.x * kMaxIv;
+  __shared__ uint32_t s_count;
+  __shared__ uint64_t s_hit;  // first probe position (relative) that may sit inside a long run
+  __shared__ uint64_t s_edge;
+  if (tid == 0) s_count = 0;
+  const uint64_t n = B.end - B.start;
+  if (n < (uint64_t)kSameLetter + kTailNoMatch + 2) {
+    if (tid == 0) ivCount[blockIdx.x] = 0;
+    return;
+  }
+  const uint64_t stopAbs = B.end - kTailLiterals;
+  // a run longer than MaxSameLetter (65299) covers three consecutive multiples of 16384
+  const uint64_t nprobe = (n + 16383) / 16384;
+  uint64_t from = 0;  // relative position from which to look for the next run
+  __syncthreads();
+  while (true) {
+    if (tid == 0) s_hit = kNone;
+    __syncthreads();
+    for (uint64_t k = tid; k + 2 < nprobe; k += blockDim.x) {
+      const uint64_t p = k * 16384;
+      if (p < from) continue;
+      const uint8_t v = in[B.start + p];
+      if (in[B.start + p + 16384] == v && in[B.start + p + 32768] == v) atomicMin((unsigned long long*)&s_hit, p);
+    }
+    __syncthreads();
+    const uint64_t hit = s_hit;
+    if (hit == kNone) break;
+    const uint8_t v = in[B.start + hit];
+    // run end e: first position > hit with a different byte (or block end)
+    if (tid == 0) s_edge = n;
+    __syncthreads();
+    for (uint64_t base = hit; base < n; base += blockDim.x * 16) {
+      bool found = false;
+      for (uint32_t j = 0; j < 16; j++) {
+        const uint64_t q = base + (uint64_t)tid * 16 + j;
+        if (q < n && in[B.start + q] != v) { atomicMin((unsigned long long*)&s_edge, q); found = true; break; }
+      }
+      (void)found;
+      __syncthreads();
+      if (s_edge != n) break;
+      __syncthreads();
+    }
+    __syncthreads();
+    const uint64_t eRel = s_edge;
+    __syncthreads();
+    // run start r: scan left; may continue into the previous block when the block has lookback
+    const bool canLookLeft = B.prev != kNoBlock;
+    if (tid == 0) s_edge = kNone;  // holds (hit - r) once found
+    __syncthreads();
+    const uint64_t leftLimit = canLookLeft ? (hit + 1) : hit;  // how far left we may step from hit
+    for (uint64_t base = 1; base <= leftLimit; base += blockDim.x * 16) {
+      for (uint32_t j = 0; j < 16; j++) {
+        const uint64_t back = base + (uint64_t)tid * 16 + j;
+        if (back <= leftLimit && in[B.start + hit - back] != v) {
+          atomicMin((unsigned long long*)&s_edge, back);
+          break;
+        }
+      }
+      __syncthreads();
+      if (s_edge != kNone) break;
+      __syncthreads();
+    }
+    __syncthreads();
+    const uint64_t backHit = s_edge;  // first step left that leaves the run (kNone: none within limit)
+    __syncthreads();
+    if (tid == 0) {
+      // run start r (relative); only whether it precedes the block start matters beyond that
+      const bool beforeStart = canLookLeft && backHit == kNone;
+      const uint64_t rRel = backHit == kNone ? 0 : hit - backHit + 1;
+      const uint64_t a = beforeStart ? B.start : B.start + rRel + 1;
+      const uint64_t eAbs = B.start + eRel;
+      const uint64_t lim = eAbs < stopAbs ? eAbs : stopAbs;
+      if (a + kTailNoMatch <= B.end && lim > a) {
+        const uint64_t La = lim - a;
+        if (La > kSameLetter && s_count < kMaxIv) {
+          Interval t;
+          t.lo = a + 1;
+          t.hi = a + 1 + (La - kSameLetter);
+          t.a = a;
+          t.La = La;
+          iv[s_count] = t;
+          s_count = s_count + 1;
+        }
+      }
+    }
+    __syncthreads();
+    from = eRel;  // continue after this run
+    if (from >= n) break;
+  }
+  __syncthreads();
+  if (tid == 0) ivCount[blockIdx.x] = s_count;
+}
+
+// ================================================================================================
+// k_sort: one 1024-thread workgroup per segment.  Sorts the inserted positions of the window
+// [w0, s1) by (key, position) with a stable LSD radix sort over the four key bytes.  After the
+// sort, the candidates of target p are the entries just below p's slot with the same key --
+// exactly the reference's previousExact chain of p, nearest first.
+// Elements are (key, position - w0) pairs in two ping-pong buffers.
+// ================================================================================================
+constexpr int kSortThreads = 1024;
+constexpr int kSortWaves = kSortThreads / 64;
+
+__global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                       const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                       const uint32_t* __restrict__ ivCount, uint2* __restrict__ bufA,
+                                                       uint2* __restrict__ bufB, uint32_t* __restrict__ rank)
+{
+  __shared__ uint32_t hist[kSortWaves][256];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
+  __shared__ uint32_t nEx;
+
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+
+  // positions excluded from insertion: shortcut intervals of this block and of the previous one
+  if (tid == 0) {
+    uint32_t k = 0;
+    const uint32_t blkIds[2] = {B.prev, S.block};
+    for (int t = 0; t < 2; t++) {
+      if (blkIds[t] == kNoBlock) continue;
+      const Interval* iv = ivAll + (uint64_t)blkIds[t] * kMaxIv;
+      for (uint32_t j = 0; j < ivCount[blkIds[t]]; j++) {
+        uint64_t lo = iv[j].lo > S.w0 ? iv[j].lo : S.w0;
+        uint64_t hi = iv[j].hi < S.s1 ? iv[j].hi : S.s1;
+        if (lo < hi) { exLo[k] = lo; exHi[k] = hi; k++; }
+      }
+    }
+    nEx = k;
+  }
+  __syncthreads();
+  const uint32_t ne = nEx;
+  uint64_t excluded = 0;
+  for (uint32_t j = 0; j < ne; j++) excluded += exHi[j] - exLo[j];
+
+  uint2* src = bufA + S.elemOff;
+  uint2* dst = bufB + S.elemOff;
+  const uint32_t W = (uint32_t)(S.s1 - S.w0);
+  const uint32_t E = W - (uint32_t)excluded;
+
+  // 1. elements in position order (intervals compacted out)
+  for (uint32_t r = tid; r < W; r += kSortThreads) {
+    const uint64_t q = S.w0 + r;
+    uint32_t idx = r;
+    bool skip = false;
+    for (uint32_t j = 0; j < ne; j++) {
+      if (q >= exHi[j]) idx -= (uint32_t)(exHi[j] - exLo[j]);
+      else if (q >= exLo[j]) skip = true;
+    }
+    if (!skip) src[idx] = make_uint2(gload4(in, q), r);
+  }
+  __syncthreads();
+
+  // 2. four stable counting passes, least significant key byte first
+  const uint32_t chunk = (((E + kSortWaves - 1) / kSortWaves) + 63) & ~63u;
+  const uint32_t b0 = wave * chunk < E ? wave * chunk : E;
+  const uint32_t b1 = b0 + chunk < E ? b0 + chunk : E;
+  for (int pass = 0; pass < 4; pass++) {
+    const uint32_t sh = pass * 8;
+    for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
+    __syncthreads();
+    for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&hist[wave][(src[i].x >> sh) & 255], 1u);
+    __syncthreads();
+    uint32_t total = 0;
+    if (tid < 256) {
+      for (int w = 0; w < kSortWaves; w++) {
+        const uint32_t c = hist[w][tid];
+        hist[w][tid] = total;
+        total += c;
+      }
+      const uint32_t incl = wave_incl_scan_add(total);
+      if (lane == 63) wsum[wave] = incl;
+      total = incl - total;  // exclusive within this wave
+    }
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t base = total;
+      for (uint32_t w = 0; w < wave; w++) base += wsum[w];
+      for (int w = 0; w < kSortWaves; w++) hist[w][tid] += base;
+    }
+    __syncthreads();
+    for (uint32_t base = b0; base < b1; base += 64) {
+      const uint32_t i = base + lane;
+      const bool valid = i < b1;
+      const uint2 e = valid ? src[i] : make_uint2(0u, 0u);
+      const uint32_t d = (e.x >> sh) & 255;
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint64_t m = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? m : ~m;
+      }
+      if (valid) {
+        const uint32_t rk = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        const uint32_t off = hist[wave][d];
+        dst[off + rk] = e;
+        if (rk == 0) hist[wave][d] = off + (uint32_t)__popcll(peers);
+      }
+    }
+    __syncthreads();
+    uint2* t = src;
+    src = dst;
+    dst = t;
+  }
+  // after four passes the sorted elements are back in bufA
+  // 3. slot of every target position
+  for (uint32_t s = tid; s < E; s += kSortThreads) {
+    const uint64_t q = S.w0 + src[s].y;
+    if (q >= S.s0) rank[S.rankOff + (q - S.s0)] = s;
+  }
+}
+
+// ================================================================================================
+// k_find: longest match per target position.  One workgroup per segment; wavefronts take chunks
+// of 64 consecutive positions and walk them in order.  For each position the wavefront scores
+// 64 candidates of the sorted key group per step (nearest first), lanes reject a candidate with a
+// single 4-byte compare at the length it would have to reach (the reference's phase 1), and the
+// survivors compute their exact common prefix.
+//
+//  maxChain >= 65535 ("-9"): result = longest common prefix over all candidates, nearest on ties
+//      (equivalent to the reference's strictly-improving walk).  Position p+1 starts from the
+//      known match (dist d, len L-1) of position p, so long repeats are not re-extended.
+//  maxChain <  65535: the reference's step limit counts strict improvements ("records") along the
+//      chain; each 64-candidate step resolves its records with a wavefront prefix-max.
+// ================================================================================================
+constexpr int kFindThreads = 512;  // 8 wavefronts; each 16-lane row owns one target at a time
+
+template <bool kLds>
+struct Bytes;
+
+template <>
+struct Bytes<true> {
+  const uint32_t* w;
+  uint64_t base;
+  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const { return lload4(w, (uint32_t)(pos - base)); }
+};
+
+template <>
+struct Bytes<false> {
+  const uint8_t* in;
+  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const { return gload4(in, pos); }
+};
+
+// exact common prefix of p and c (capped at room) if it reaches `need`, else 0
+template <class Src>
+__device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t p, uint64_t c, uint32_t need, uint32_t room)
+{
+  if (need > room) return 0;
+  if (need > 4) {
+    if (src.ld4(p + need - 4) != src.ld4(c + need - 4)) return 0;
+    for (uint32_t k = 4; k + 4 < need; k += 4)
+      if (src.ld4(p + k) != src.ld4(c + k)) return 0;
+  }
+  uint32_t k = need > 4 ? need : 4;
+  while (k < room) {
+    const uint32_t x = src.ld4(p + k) ^ src.ld4(c + k);
+    if (x) {
+      k += (uint32_t)__builtin_ctz(x) >> 3;
+      break;
+    }
+    k += 4;
+  }
+  return k < room ? k : room;
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                       const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                       const uint32_t* __restrict__ ivCount, const uint2* __restrict__ elemAll,
+                                                       const uint32_t* __restrict__ rankAll, uint32_t maxChain,
+                                                       uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                       uint64_t matchBase)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t win[];
+  __shared__ uint32_t s_next;
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, row = lane >> 4, li = lane & 15;
+  const uint2* elem = elemAll + S.elemOff;
+  const uint32_t* rank = rankAll + S.rankOff;
+  const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
+  const uint32_t niv = ivCount[S.block];
+
+  if (tid == 0) s_next = 0;
+  Bytes<kLds> src;
+  if constexpr (kLds) {
+    const uint32_t words = (uint32_t)((B.end - S.w0 + 8 + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
+    src.w = win;
+    src.base = S.w0;
+  } else {
+    src.in = in;
+  }
+  __syncthreads();
+
+  // chain cut (lookback re-insertion of B.cut, smallz4.h:614-624): applies only if the previous
+  // block inserted that position (it is not inside one of its shortcut intervals)
+  uint64_t cut = B.cut;
+  uint32_t cutHash = 0;
+  if (cut != kNone) {
+    const Interval* pv = ivAll + (uint64_t)B.prev * kMaxIv;
+    if (in_iv(pv, ivCount[B.prev], cut)) cut = kNone;
+    else cutHash = ref_hash(gload4(in, cut));
+  }
+  const Interval* pvIv = B.prev != kNoBlock ? ivAll + (uint64_t)B.prev * kMaxIv : iv;
+  const uint32_t pvN = B.prev != kNoBlock ? ivCount[B.prev] : 0u;
+  const uint64_t stopAbs = B.end - kTailLiterals;
+  const bool unlimited = maxChain >= 65535u;
+  const uint32_t nTargets = (uint32_t)(S.s1 - S.s0);
+  const uint32_t rowBase = row << 4;
+
+  while (true) {
+    uint32_t chunkIdx = 0;
+    if (lane == 0) chunkIdx = atomicAdd(&s_next, 1u);
+    chunkIdx = rdlane(chunkIdx, 0);
+    const uint32_t first = chunkIdx * 64;
+    if (first >= nTargets) break;
+    const uint32_t cnt = nTargets - first < 64 ? nTargets - first : 64;
+    const uint32_t myRank = lane < cnt ? rank[first + lane] : 0u;
+    const uint32_t rowCnt = cnt > rowBase ? (cnt - rowBase < 16 ? cnt - rowBase : 16) : 0;
+
+    // per-row state (replicated over the row's 16 lanes)
+    uint32_t j = 0;  // target index inside the row
+    bool needInit = true, done = false, isIv = false;
+    uint64_t p = 0, lb = 0;
+    uint32_t key = 0, room = 0, bestLen = 0, bestDist = 0, steps = 0;
+    int64_t slot = 0;
+    uint32_t carryLen = 0, carryDist = 0;
+    uint32_t resLen = 0, resDist = 0;  // lane rowBase+t holds the result of target first+rowBase+t
+
+    while (true) {
+      const bool live = j < rowCnt;
+      if (__ballot(live) == 0) break;
+      const uint32_t rCur = __shfl(myRank, (int)(rowBase + (j & 15)), 64);
+      if (live && needInit) {
+        needInit = false;
+        done = false;
+        isIv = false;
+        p = S.s0 + first + rowBase + j;
+        for (uint32_t k = 0; k < niv; k++)
+          if (p >= iv[k].lo && p < iv[k].hi) {
+            // shortcut interval: the reference copies the predecessor's match, minus one
+            isIv = true;
+            bestLen = (uint32_t)(iv[k].La - (p - iv[k].a));
+            bestDist = 1;
+          }
+        if (isIv) {
+          done = true;
+        } else {
+          key = src.ld4(p);
+          room = (uint32_t)(stopAbs - p);
+          lb = p > kWindow ? p - kWindow : 0;
+          if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
+          slot = (int64_t)rCur - 1;
+          if (unlimited) {
+            bestLen = 0;
+            bestDist = 0;
+            // the candidate at the previous target's best distance matches exactly one byte less
+            if (carryLen >= 5) {
+              const uint64_t c = p - carryDist;
+              if (c >= lb && !(niv && in_iv(iv, niv, c)) && !(pvN && in_iv(pvIv, pvN, c))) {
+                bestLen = carryLen - 1;
+                bestDist = carryDist;
+              }
+            }
+          } else {
+            bestLen = 1;
+            bestDist = 0;
+            steps = maxChain;
+          }
+        }
+      }
+      // one step: 16 candidates of the row's key group, nearest first
+      const bool act = live && !done;
+      bool valid = false;
+      uint32_t got = 0, dist = 0;
+      if (act) {
+        const int64_t sl = slot - (int64_t)li;
+        if (sl >= 0) {
+          const uint2 e = elem[sl];
+          const uint64_t c = S.w0 + e.y;
+          valid = e.x == key && c >= lb;
+          if (valid) {
+            dist = (uint32_t)(p - c);
+            if (unlimited) {
+              if (dist != bestDist) {
+                const uint32_t need = dist < bestDist ? bestLen : bestLen + 1;
+                got = prefix_if_at_least(src, p, c, need < 4 ? 4 : need, room);
+                if (got < need) got = 0;
+              }
+            } else {
+              got = prefix_if_at_least(src, p, c, bestLen + 1 < 4 ? 4 : bestLen + 1, room);
+              if (got <= bestLen) got = 0;
+            }
+          }
+        }
+      }
+      const uint32_t rowValid = (uint32_t)(__ballot(valid) >> rowBase) & 0xFFFFu;
+      if (unlimited) {
+        // longest, then nearest (lower lane = nearer candidate)
+        const uint32_t top = row_max(got ? (got << 4) | (15u - li) : 0u);
+        const uint32_t wdist = __shfl(dist, (int)(rowBase + 15u - (top & 15u)), 64);
+        const uint32_t farDist = __shfl(dist, (int)(rowBase + 15u), 64);
+        if (act) {
+          if (top) {
+            const uint32_t tl = top >> 4;
+            if (tl > bestLen || (tl == bestLen && wdist < bestDist)) {
+              bestLen = tl;
+              bestDist = wdist;
+            }
+          }
+          if (rowValid != 0xFFFFu) done = true;                           // key group / window exhausted
+          else if (bestLen >= room && farDist >= bestDist) done = true;   // nothing left can win
+          slot -= 16;
+        }
+      } else {
+        // strict improvements in chain order ("records"); the reference stops after maxChain of them
+        const uint32_t incl = row_scan_max(got);
+        const uint32_t excl = dpp<kRowShr + 1>(incl);  // row lane 0 reads outside its row: 0 (keep unconditional: DPP must not read a masked-off lane)
+        const bool rec = got > bestLen && got > excl;
+        const uint32_t rowRec = (uint32_t)(__ballot(rec) >> rowBase) & 0xFFFFu;
+        const uint32_t nrec = (uint32_t)__popc(rowRec);
+        uint32_t sel = 0;
+        if (nrec) {
+          if (nrec >= steps) {
+            uint32_t m = rowRec;
+            for (uint32_t k = 1; k < steps; k++) m &= m - 1;
+            sel = (uint32_t)__builtin_ctz(m);
+          } else {
+            sel = 31u - (uint32_t)__builtin_clz(rowRec);
+          }
+        }
+        const uint32_t selGot = __shfl(got, (int)(rowBase + sel), 64);
+        const uint32_t selDist = __shfl(dist, (int)(rowBase + sel), 64);
+        if (act) {
+          if (nrec) {
+            bestLen = selGot;
+            bestDist = selDist;
+            if (nrec >= steps) done = true;
+            else steps -= nrec;
+          }
+          if (rowValid != 0xFFFFu || bestLen >= room) done = true;
+          slot -= 16;
+        }
+      }
+      if (live && done) {
+        if (!isIv && bestDist == 0) bestLen = 0;  // no candidate: the reference never searched here
+        if (li == j) {
+          resLen = bestLen;
+          resDist = bestDist;
+        }
+        carryLen = isIv ? 0u : bestLen;
+        carryDist = bestDist;
+        j++;
+        needInit = true;
+      }
+    }
+    if (lane < cnt) {
+      const uint64_t idx = S.s0 + first + lane - matchBase;
+      mlen[idx] = resLen;
+      mdist[idx] = (uint16_t)resDist;
+    }
+  }
+}
+
+// ================================================================================================
+// k_parse: one wavefront per block.
+//   1. greedy/lazy levels: the reference's skip scan decides which searched positions it keeps
+//      (smallz4.h:726-744);
+//   2. levels > 3: backward optimal parse (estimateCosts, smallz4.h:376-472).  Costs of the last
+//      kRing positions live in an LDS ring, older ones in HBM; per position the wavefront scores
+//      64 match lengths per step and reduces (cost, -length) with a wave minimum;
+// ================================================================================================
+constexpr int kRing = 4096;
+
+__device__ __forceinline__ uint32_t len_extra(uint32_t len)
+{
+  return len < 19 ? 3u : 4u + (len - 19) / 255;
+}
+
+__global__ __launch_bounds__(64) void k_parse(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                              const Interval* __restrict__ ivAll, const uint32_t* __restrict__ ivCount,
+                                              uint32_t maxChain, uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                              uint64_t matchBase, uint32_t* __restrict__ costAll, int* __restrict__ status)
+{
+  __shared__ uint32_t ring[kRing];
+  const Block B = blocks[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t n = B.end - B.start;
+  uint32_t* L = mlen + (B.start - matchBase);
+  const uint16_t* D = mdist + (B.start - matchBase);
+  uint32_t* cost = costAll + (B.start - matchBase) + blockIdx.x;  // n + 1 entries per block
+  const Interval* iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
+  const uint32_t niv = ivCount[blockIdx.x];
+  const bool stored = maxChain == 0;
+  const bool legacy = (B.flags & kBlkLegacy) != 0;
+  const uint64_t lastSearch = n >= (uint64_t)kTailNoMatch ? n - kTailNoMatch : 0;  // inclusive, relative
+
+  // positions the reference never searched keep length 0 (it leaves them default-constructed)
+  if (!stored && n >= (uint64_t)kTailNoMatch) {
+    for (uint64_t i = lastSearch + 1 + lane; i < n; i += 64) L[i] = 0;
+  } else if (!stored) {
+    for (uint64_t i = lane; i < n; i += 64) L[i] = 0;
+  }
+
+  // ---- 1. greedy / lazy skip scan ---------------------------------------------------------------
+  if (!stored && maxChain <= (uint32_t)kLazyMax && n >= (uint64_t)kTailNoMatch) {
+    if (niv) {
+      if (lane == 0) atomicOr(status, 1);  // shortcut interplay with skipping: not on this path
+    }
+    // one lane replays the reference's bookkeeping over an LDS copy of each 64-position chunk
+    __shared__ uint32_t chunkL[64];
+    uint64_t skip = 0;
+    bool lazyEval = false;
+    for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
+      const uint64_t i = c0 + lane;
+      const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
+      chunkL[lane] = i <= lastSearch ? ld_fresh(&L[i]) : 0u;
+      __syncthreads();
+      if (lane == 0) {
+        for (uint32_t k = 0; k < cnt; k++) {
+          const uint32_t lk = chunkL[k];
+          // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
+          if (lk >= (uint32_t)kMinMatch) {
+            bool search = true;
+            if (skip > 0) {
+              skip--;
+              search = lazyEval;  // a pending lazy evaluation searches one more position
+              lazyEval = false;
+            }
+            if (search) {
+              lazyEval = (skip == 0);
+              skip = lk;
+            } else {
+              chunkL[k] = 0;  // never searched by the reference
+            }
+          }
+        }
+      }
+      __syncthreads();
+      if (i <= lastSearch) L[i] = chunkL[lane];
+      __syncthreads();
+    }
+    __threadfence_block();
+  }
+
+  // ---- 2. backward optimal parse ---------------------------------------------------------------
+  if (!stored && n > (uint64_t)kTailNoMatch && maxChain > (uint32_t)kGreedyMax) {
+    for (uint64_t j = n - kTailLiterals + lane; j <= n; j += 64) {
+      ring[j & (kRing - 1)] = 0;
+      cost[j] = 0;
+    }
+    __threadfence_block();
+    uint32_t lits = kTailLiterals;
+    uint32_t costNext = 0;  // cost[i + 1]
+    for (int64_t hi = (int64_t)n - 1 - kTailLiterals; hi >= 0; hi -= 64) {
+      const int64_t lo = hi - 63 > 0 ? hi - 63 : 0;
+      const int64_t iMine = hi - (int64_t)lane;
+      const uint32_t myL = iMine >= lo ? ld_fresh(&L[iMine]) : 0;
+      const uint32_t myD = iMine >= lo ? D[iMine] : 0;
+      uint32_t myBest = 1, myCost = 0;
+      for (int64_t i = hi; i >= lo; i--) {
+        const int k = (int)(hi - i);
+        const uint32_t Lk = rdlane(myL, (uint32_t)k);
+        const uint32_t Dk = rdlane(myD, (uint32_t)k);
+        lits++;
+        uint32_t minCost = costNext + 1;
+        if (lits == 15 || (lits >= 15 + 255 && (lits - 15) % 255 == 0)) minCost++;
+        uint32_t best = 1;
+        if (Lk >= kSameLetter && Dk == 1) {
+          const uint64_t j = (uint64_t)i + Lk;
+          const uint32_t cj = Lk < kRing - 64 ? ring[j & (kRing - 1)]
+                                              : ld_fresh(&cost[j]);
+          best = Lk;
+          minCost = cj + 4 + (Lk - 19) / 255;
+        } else if (Lk >= (uint32_t)kMinMatch) {
+          for (uint32_t b = kMinMatch; b <= Lk; b += 64) {
+            const uint32_t len = b + lane;
+            uint32_t keyv = 0xFFFFFFFFu;
+            if (len <= Lk) {
+              const uint64_t j = (uint64_t)i + len;
+              const uint32_t cj = len < kRing - 64 ? ring[j & (kRing - 1)]
+                                                   : ld_fresh(&cost[j]);
+              const uint32_t tot = cj + len_extra(len);
+              keyv = (tot << 6) | (63u - lane);  // min cost, then longest
+            }
+            const uint32_t kmin = wave_min_fast(keyv);
+            const uint32_t cmin = kmin >> 6;
+            if (kmin != 0xFFFFFFFFu && cmin <= minCost) {
+              minCost = cmin;
+              best = b + (63u - (kmin & 63u));
+            }
+          }
+        }
+        if (lane == 0) ring[(uint64_t)i & (kRing - 1)] = minCost;
+        costNext = minCost;
+        if (lane == (uint32_t)k) { myBest = best; myCost = minCost; }
+        if (best != 1) lits = 0;
+      }
+      if (iMine >= lo) {
+        L[iMine] = myBest;
+        cost[iMine] = myCost;
+      }
+      __threadfence_block();
+    }
+  }
+
+}
+
+// ================================================================================================
+// k_tokens: one wavefront per block walks the parse forward exactly like selectBestMatches
+// (smallz4.h:259-371) and records one token per (literal run, match): 16 bytes each.  The walk
+// keeps the current and the next 64-position window of chosen lengths in registers and jumps over
+// literal stretches with one ballot.  It also sizes the encoding and makes the stored/compressed
+// decision of smallz4.h:764-771.
+// ================================================================================================
+__device__ __forceinline__ uint64_t token_bytes(uint64_t lits, uint32_t mlen, bool last)
+{
+  uint64_t b = 1 + lits + (lits >= 15 ? (lits - 15) / 255 + 1 : 0);
+  if (!last) {
+    const int64_t mcode = (int64_t)mlen - kMinMatch;
+    b += 2 + (mcode >= 15 ? (uint64_t)(mcode - 15) / 255 + 1 : 0);
+  }
+  return b;
+}
+
+__global__ __launch_bounds__(64) void k_tokens(const Block* __restrict__ blocks, uint32_t maxChain,
+                                               const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                               uint64_t matchBase, Token* __restrict__ tokAll, uint32_t* __restrict__ ntokOut,
+                                               uint32_t* __restrict__ blockBytes)
+{
+  const Block B = blocks[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t n = B.end - B.start;
+  const uint32_t* L = mlen + (B.start - matchBase);
+  const uint16_t* D = mdist + (B.start - matchBase);
+  Token* tok = tokAll + B.tokOff;
+  const bool stored = maxChain == 0;
+  const bool legacy = (B.flags & kBlkLegacy) != 0;
+  uint64_t enc = 0;
+  uint32_t ntok = 0;
+  if (!stored) {
+    uint64_t pos = 0, litFrom = 0, lits = 0;
+    uint64_t wbase = 0;
+    uint32_t wL = lane < n ? L[lane] : 0u, wD = lane < n ? D[lane] : 0u;
+    uint32_t nL = 64 + lane < n ? L[64 + lane] : 0u, nD = 64 + lane < n ? D[64 + lane] : 0u;
+    while (pos < n) {
+      if (pos >= wbase + 64) {
+        if (pos < wbase + 128) {
+          wbase += 64;
+          wL = nL;
+          wD = nD;
+        } else {
+          wbase = pos & ~63ull;
+          wL = wbase + lane < n ? L[wbase + lane] : 0u;
+          wD = wbase + lane < n ? D[wbase + lane] : 0u;
+        }
+        const uint64_t nb = wbase + 64 + lane;
+        nL = nb < n ? L[nb] : 0u;
+        nD = nb < n ? D[nb] : 0u;
+      }
+      const uint32_t rel = (uint32_t)(pos - wbase);
+      const uint64_t mm = __ballot(wL > 1u) & (~0ull << rel);
+      if (mm == 0) {
+        const uint64_t end = wbase + 64 < n ? wbase + 64 : n;
+        if (lits == 0) litFrom = pos;
+        lits += end - pos;
+        pos = end;
+        continue;
+      }
+      const uint32_t f = (uint32_t)__builtin_ctzll(mm);
+      if (f > rel) {
+        if (lits == 0) litFrom = pos;
+        lits += f - rel;
+      }
+      const uint32_t Lm = rdlane(wL, f), Dm = rdlane(wD, f);
+      if (lane == 0) tok[ntok] = Token{(uint32_t)(lits ? litFrom : 0), (uint32_t)lits, Lm, Dm};
+      ntok++;
+      enc += token_bytes(lits, Lm, false);
+      lits = 0;
+      pos = wbase + f + Lm;
+    }
+    // the block always ends with literals (the last five positions are never matched)
+    if (lane == 0) tok[ntok] = Token{(uint32_t)litFrom, (uint32_t)lits, 0u, kTokLast};
+    ntok++;
+    enc += token_bytes(lits, 0, true);
+  }
+  const bool useEnc = (enc < n && !stored) || legacy;
+  const uint32_t bytes = (uint32_t)(useEnc ? enc : n);
+  if (lane == 0) {
+    ntokOut[blockIdx.x] = useEnc ? ntok : 0u;
+    blockBytes[blockIdx.x] = (useEnc ? 0u : 0x80000000u) | (bytes + 4u);
+  }
+}
+
+// ================================================================================================
+// k_scan + k_assemble: frame = header, then each block's word + payload (or its raw bytes when
+// the block is stored), then the end mark.
+// ================================================================================================
+__global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ blockBytes, uint32_t nblocks,
+                                               uint64_t* __restrict__ offsets)
+{
+  __shared__ uint64_t s_carry;
+  __shared__ uint32_t s_w[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < nblocks; base += 1024) {
+    const uint32_t i = base + tid;
+    const uint32_t v = i < nblocks ? (blockBytes[i] & 0x7FFFFFFFu) : 0u;
+    const uint32_t incl = wave_incl_scan_add(v);
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint64_t pre = s_carry;
+    for (uint32_t w = 0; w < wave; w++) pre += s_w[w];
+    if (i < nblocks) offsets[i] = pre + incl - v;
+    __syncthreads();
+    if (tid == 1023) s_carry = pre + incl;
+    __syncthreads();
+  }
+  if (tid == 0) offsets[nblocks] = s_carry;
+}
+
+// k_write: one 256-thread workgroup per block writes the block word and either the raw bytes
+// (stored block) or its tokens: token offsets by a workgroup scan of token sizes, then every
+// thread encodes one token (smallz4.h:310-367) straight into the frame.
+__global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                               const Token* __restrict__ tokAll, const uint32_t* __restrict__ ntokAll,
+                                               const uint32_t* __restrict__ blockBytes, const uint64_t* __restrict__ offsets,
+                                               uint8_t* __restrict__ out, uint64_t headerLen)
+{
+  __shared__ uint64_t s_w[4];
+  __shared__ uint64_t s_carry;
+  const Block B = blocks[blockIdx.x];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t bb = blockBytes[blockIdx.x];
+  const bool raw = (bb & 0x80000000u) != 0;
+  const uint32_t bytes = (bb & 0x7FFFFFFFu) - 4u;
+  uint8_t* dst = out + headerLen + offsets[blockIdx.x];
+  if (tid == 0) {
+    const uint32_t word = bytes | (raw ? 0x80000000u : 0u);
+    dst[0] = (uint8_t)word;
+    dst[1] = (uint8_t)(word >> 8);
+    dst[2] = (uint8_t)(word >> 16);
+    dst[3] = (uint8_t)(word >> 24);
+    s_carry = 0;
+  }
+  dst += 4;
+  const uint8_t* src = in + B.start;
+  if (raw) {
+    for (uint64_t k = tid; k < bytes; k += 256) dst[k] = src[k];
+    return;
+  }
+  const Token* tok = tokAll + B.tokOff;
+  const uint32_t ntok = ntokAll[blockIdx.x];
+  __syncthreads();
+  for (uint32_t base = 0; base < ntok; base += 256) {
+    const uint32_t t = base + tid;
+    Token T{0, 0, 0, 0};
+    uint64_t sz = 0;
+    const bool last = t < ntok && (tok[t].dist & kTokLast);
+    if (t < ntok) {
+      T = tok[t];
+      sz = token_bytes(T.lits, T.mlen, last);
+    }
+    // workgroup exclusive scan of token sizes
+    uint64_t incl = sz;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t o = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += o;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint64_t off = s_carry + incl - sz;
+    for (uint32_t w = 0; w < wave; w++) off += s_w[w];
+    __syncthreads();
+    if (tid == 255) s_carry = off + sz;
+    if (t < ntok) {
+      uint8_t* o = dst + off;
+      const int64_t mcode = last ? 0 : (int64_t)T.mlen - kMinMatch;
+      const uint8_t tk = (uint8_t)(mcode < 15 ? mcode : 15);
+      uint64_t lits = T.lits;
+      if (lits < 15) {
+        *o++ = (uint8_t)(tk | (lits << 4));
+      } else {
+        *o++ = (uint8_t)(tk | 0xF0);
+        uint64_t v = lits - 15;
+        while (v >= 255) { *o++ = 255; v -= 255; }
+        *o++ = (uint8_t)v;
+      }
+      const uint8_t* ls = src + T.litFrom;
+      for (uint64_t k = 0; k < lits; k++) o[k] = ls[k];
+      o += lits;
+      if (!last) {
+        const uint32_t dd = T.dist & 0xFFFFu;
+        o[0] = (uint8_t)(dd & 0xFF);
+        o[1] = (uint8_t)(dd >> 8);
+        o += 2;
+        if (mcode >= 15) {
+          uint64_t v = (uint64_t)(mcode - 15);
+          while (v >= 255) { *o++ = 255; v -= 255; }
+          *o++ = (uint8_t)v;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
+void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, hipStream_t s)
+{
+  if (nblocks) hipLaunchKernelGGL(k_runs, dim3(nblocks), dim3(256), 0, s, in, blocks, iv, ivCount);
+}
+
+void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
+                 const uint32_t* ivCount, uint2* elemA, uint2* elemB, uint32_t* rank, hipStream_t s)
+{
+  if (nsegs)
+    hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB, rank);
+}
+
+uint32_t find_lds_bytes() { return 65536 + 16; }
+
+void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
+                 const uint32_t* ivCount, const uint2* elem, const uint32_t* rank, uint32_t maxChain, uint32_t* mlen,
+                 uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
+{
+  if (!nsegs) return;
+  if (ldsWindow) {
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)k_find<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
+                       elem, rank, maxChain, mlen, mdist, matchBase);
+  } else {
+    hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, elem, rank,
+                       maxChain, mlen, mdist, matchBase);
+  }
+}
+
+void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const Interval* iv, const uint32_t* ivCount,
+                  uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase, uint32_t* cost, int* status,
+                  hipStream_t s)
+{
+  if (nblocks)
+    hipLaunchKernelGGL(k_parse, dim3(nblocks), dim3(64), 0, s, in, blocks, iv, ivCount, maxChain, mlen, mdist, matchBase, cost,
+                       status);
+}
+
+void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
+                 const uint16_t* mdist, uint64_t matchBase, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
+                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s)
+{
+  if (!nblocks) return;
+  hipLaunchKernelGGL(k_tokens, dim3(nblocks), dim3(64), 0, s, blocks, maxChain, mlen, mdist, matchBase, tokens, ntok, blockBytes);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, blockBytes, nblocks, offsets);
+  hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(256), 0, s, in, blocks, tokens, ntok, blockBytes, offsets, out, headerLen);
+}
+
+}  // namespace sz4
