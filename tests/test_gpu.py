@@ -166,3 +166,19 @@ def test_cpp_dropin_program(tmp_path):
         r = subprocess.run([str(exe), str(level), str(legacy)], input=data, capture_output=True, check=True)
         chain = 65535 if level == 9 else level
         assert r.stdout == pyoracle.oz_lz4(data, chain, b"", bool(legacy))
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "smallz4_on_amd")),
+                    reason="reference CLI not rebuilt against the drop-in header")
+def test_reference_cli_rebuilt_on_dropin(tmp_path):
+    """The reference's own smallz4.cpp, compiled unchanged against include/compat/smallz4.h,
+    produces the same files as the reference binary (both built by oracle/Makefile)."""
+    amd = os.path.join(ROOT, "oracle", "_ref", "smallz4_on_amd")
+    ref = os.path.join(ROOT, "oracle", "_ref", "smallz4")
+    src = tmp_path / "in.txt"
+    src.write_bytes(synth.enwik8_like(6 << 20, seed=19))
+    for flags in (["-9"], ["-6"], ["-2"], ["-0"], ["-9", "-l"]):
+        a, b = tmp_path / "a.lz4", tmp_path / "b.lz4"
+        subprocess.run([amd, "-f", *flags, str(src), str(a)], check=True)
+        subprocess.run([ref, "-f", *flags, str(src), str(b)], check=True)
+        assert a.read_bytes() == b.read_bytes(), flags
