@@ -197,9 +197,13 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   mark(c, 1, s);
   if (maxChain > 0) launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
   mark(c, 2, s);
-  if (maxChain > 0)
-    launch_find(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain, c->mlen.as<uint32_t>(),
-                c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
+  if (maxChain > 0) {
+    // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
+    if (maxChain > 0 && (e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)))
+      return c->fail(SZ4_E_DEVICE, "clear matches", e);
+    launch_find(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
+  }
   mark(c, 3, s);
   if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   launch_parse(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(),

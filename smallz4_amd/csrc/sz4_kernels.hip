@@ -372,10 +372,43 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
     src = dst;
     dst = t;
   }
-  // after four passes the sorted elements are back in bufA
-  // 3. slot of every target position
-  for (uint32_t s = tid; s < E; s += kSortThreads) {
-    const uint64_t q = S.w0 + src[s].y;
+  // after four passes the sorted elements are back in bufA; bufB is free and receives the
+  // compact per-slot arrays the sorted-order search reads: window position and the slot where its
+  // key group starts (u16 each when the window fits 16 bits, u32 otherwise)
+  // 3. group starts by a workgroup max-scan over contiguous slot ranges; slot of every target
+  const uint32_t per = (E + kSortThreads - 1) / kSortThreads;
+  const uint32_t r0 = tid * per < E ? tid * per : E;
+  const uint32_t r1 = r0 + per < E ? r0 + per : E;
+  uint32_t localStart = 0;  // last group start inside [r0, r1), +1 (0 = none)
+  for (uint32_t s = r0; s < r1; s++)
+    if (s == 0 || src[s].x != src[s - 1].x) localStart = s + 1;
+  __shared__ uint32_t s_scan[kSortThreads];
+  s_scan[tid] = localStart;
+  __syncthreads();
+  for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
+    const uint32_t v = tid >= d ? s_scan[tid - d] : 0u;
+    __syncthreads();
+    if (v > s_scan[tid]) s_scan[tid] = v;
+    __syncthreads();
+  }
+  uint32_t gs = tid ? s_scan[tid - 1] : 0u;  // inclusive max of earlier threads, +1
+  gs = gs ? gs - 1 : 0;
+  const bool small = W <= 65536u;  // == compact_small(S)
+  uint16_t* pos16 = reinterpret_cast<uint16_t*>(bufB + S.elemOff);
+  uint16_t* gs16 = pos16 + E;
+  uint32_t* pos32 = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
+  uint32_t* gs32 = pos32 + E;
+  for (uint32_t s = r0; s < r1; s++) {
+    const uint2 e = src[s];
+    if (s == 0 || e.x != src[s - 1].x) gs = s;
+    if (small) {
+      pos16[s] = (uint16_t)e.y;
+      gs16[s] = (uint16_t)gs;
+    } else {
+      pos32[s] = e.y;
+      gs32[s] = gs;
+    }
+    const uint64_t q = S.w0 + e.y;
     if (q >= S.s0) rank[S.rankOff + (q - S.s0)] = s;
   }
 }
@@ -433,6 +466,157 @@ __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t 
   return k < room ? k : room;
 }
 
+// ================================================================================================
+// k_find_sorted (pass 1): one lane per target, targets taken in SORTED order.  A lane's
+// candidates are the slots just below its own inside its key group, so the 64 lanes of a
+// wavefront read neighbouring slots (coalesced) and lanes of one big group loop the same number
+// of times.  Each lane runs the reference's own nearest-first scan (smallz4.h:190-252): phase-1
+// check at the length it must reach, extension, strict improvement, step limit.  The extension is
+// capped at kLongCap bytes: a target whose best reaches the cap keeps the marker kLongMatch and is
+// finished by k_find (pass 2), which walks long repeats in text order with the carried match.
+// ================================================================================================
+constexpr uint32_t kLongCap = 32;
+constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
+
+// per-slot arrays written by k_sort: u16 when the segment's window fits 16 bits (same predicate there)
+__device__ __forceinline__ bool compact_small(const Segment& S) { return S.s1 - S.w0 <= 65536u; }
+__device__ __forceinline__ uint32_t slot_pos(const void* base, bool small, uint32_t s)
+{
+  return small ? (uint32_t)reinterpret_cast<const uint16_t*>(base)[s] : reinterpret_cast<const uint32_t*>(base)[s];
+}
+__device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32_t E, uint32_t s)
+{
+  return small ? (uint32_t)reinterpret_cast<const uint16_t*>(base)[E + s] : reinterpret_cast<const uint32_t*>(base)[E + s];
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                              const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                              const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
+                                                              uint32_t maxChain, uint32_t* __restrict__ mlen,
+                                                              uint16_t* __restrict__ mdist, uint64_t matchBase)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t win[];
+  __shared__ uint32_t s_next;
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const void* compact = compactAll + S.elemOff;
+  // number of sorted slots: window positions minus shortcut-interval positions
+  const uint32_t W = (uint32_t)(S.s1 - S.w0);
+  uint32_t excluded = 0;
+  {
+    const uint32_t ids[2] = {B.prev, S.block};
+    for (int t = 0; t < 2; t++) {
+      if (ids[t] == kNoBlock) continue;
+      const Interval* iv = ivAll + (uint64_t)ids[t] * kMaxIv;
+      for (uint32_t j = 0; j < ivCount[ids[t]]; j++) {
+        const uint64_t lo = iv[j].lo > S.w0 ? iv[j].lo : S.w0, hi = iv[j].hi < S.s1 ? iv[j].hi : S.s1;
+        if (lo < hi) excluded += (uint32_t)(hi - lo);
+      }
+    }
+  }
+  const uint32_t E = W - excluded;
+  const bool small = compact_small(S);
+
+  if (tid == 0) s_next = 0;
+  Bytes<kLds> src;
+  if constexpr (kLds) {
+    const uint32_t words = (uint32_t)((B.end - S.w0 + 8 + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
+    src.w = win;
+    src.base = S.w0;
+  } else {
+    src.in = in;
+  }
+  __syncthreads();
+
+  uint64_t cut = B.cut;
+  uint32_t cutHash = 0;
+  if (cut != kNone) {
+    const Interval* pv = ivAll + (uint64_t)B.prev * kMaxIv;
+    if (in_iv(pv, ivCount[B.prev], cut)) cut = kNone;
+    else cutHash = ref_hash(gload4(in, cut));
+  }
+  const uint64_t stopAbs = B.end - kTailLiterals;
+  const bool unlimited = maxChain >= 65535u;
+
+  while (true) {
+    uint32_t chunkIdx = 0;
+    if (lane == 0) chunkIdx = atomicAdd(&s_next, 1u);
+    chunkIdx = rdlane(chunkIdx, 0);
+    const uint32_t first = chunkIdx * 64;
+    if (first >= E) break;
+    const uint32_t slot = first + lane;
+    uint64_t p = 0;
+    uint32_t gs = 0;
+    bool active = slot < E;
+    if (active) {
+      p = S.w0 + slot_pos(compact, small, slot);
+      gs = slot_gs(compact, small, E, slot);
+      active = p >= S.s0;  // else a window-only position (previous segment / previous block)
+    }
+    if (active) {
+      const uint32_t key = src.ld4(p);
+      const uint32_t room = (uint32_t)(stopAbs - p);
+      uint64_t lb = p > kWindow ? p - kWindow : 0;
+      if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
+      const uint32_t limit = room < kLongCap ? room : kLongCap;
+      uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
+      bool isLong = false, run = true;
+      int64_t j = (int64_t)slot - 1;
+      while (run && j >= (int64_t)gs) {
+        // four candidates per trip: their loads are independent
+        uint32_t cp[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          cp[u] = j - u >= (int64_t)gs ? slot_pos(compact, small, (uint32_t)(j - u)) : 0xFFFFFFFFu;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (run) {
+            const uint64_t c = S.w0 + cp[u];
+            const uint32_t need = bestLen + 1 < 4 ? 4 : bestLen + 1;
+            if (cp[u] == 0xFFFFFFFFu || c < lb || need > room) {
+              run = false;
+            } else {
+              // phase 1: the four bytes ending at `need` decide most candidates, then the rest
+              bool same = need <= 4 || src.ld4(p + need - 4) == src.ld4(c + need - 4);
+              for (uint32_t k = 4; same && k + 4 < need; k += 4) same = src.ld4(p + k) == src.ld4(c + k);
+              if (same) {
+                // phase 2: extend up to the cap
+                uint32_t k = need;
+                bool open = true;
+                while (open && k < limit) {
+                  const uint32_t x = src.ld4(p + k) ^ src.ld4(c + k);
+                  if (x) {
+                    k += (uint32_t)__builtin_ctz(x) >> 3;
+                    open = false;
+                  } else {
+                    k += 4;
+                  }
+                }
+                if (k > limit) k = limit;
+                bestLen = k;
+                bestDist = (uint32_t)(p - c);
+                if (k >= limit && limit < room) {
+                  isLong = true;
+                  run = false;
+                } else if (--steps == 0 || bestLen >= room) {
+                  run = false;
+                }
+              }
+            }
+          }
+        }
+        j -= 4;
+      }
+      const uint64_t idx = p - matchBase;
+      mlen[idx] = isLong ? kLongMatch : (bestDist ? bestLen : 0u);
+      mdist[idx] = (uint16_t)bestDist;
+    }
+  }
+}
+
 template <bool kLds>
 __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
@@ -486,6 +670,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     const uint32_t first = chunkIdx * 64;
     if (first >= nTargets) break;
     const uint32_t cnt = nTargets - first < 64 ? nTargets - first : 64;
+    // pass 2: only targets pass 1 left marked (long matches, shortcut intervals) are searched here
+    const uint64_t myIdx = S.s0 + first + lane - matchBase;
+    const uint32_t pass1Len = lane < cnt ? mlen[myIdx] : 0u;
+    const uint32_t pass1Dist = lane < cnt ? (uint32_t)mdist[myIdx] : 0u;
+    if (__ballot(pass1Len == kLongMatch) == 0) continue;
     const uint32_t myRank = lane < cnt ? rank[first + lane] : 0u;
     const uint32_t rowCnt = cnt > rowBase ? (cnt - rowBase < 16 ? cnt - rowBase : 16) : 0;
 
@@ -496,18 +685,26 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     uint32_t key = 0, room = 0, bestLen = 0, bestDist = 0, steps = 0;
     int64_t slot = 0;
     uint32_t carryLen = 0, carryDist = 0;
-    uint32_t resLen = 0, resDist = 0;  // lane rowBase+t holds the result of target first+rowBase+t
+    uint32_t resLen = pass1Len, resDist = pass1Dist;  // lane rowBase+t holds the result of target first+rowBase+t
 
     while (true) {
       const bool live = j < rowCnt;
       if (__ballot(live) == 0) break;
       const uint32_t rCur = __shfl(myRank, (int)(rowBase + (j & 15)), 64);
+      const uint32_t curP1Len = __shfl(pass1Len, (int)(rowBase + (j & 15)), 64);
+      const uint32_t curP1Dist = __shfl(pass1Dist, (int)(rowBase + (j & 15)), 64);
       if (live && needInit) {
         needInit = false;
         done = false;
         isIv = false;
         p = S.s0 + first + rowBase + j;
-        for (uint32_t k = 0; k < niv; k++)
+        if (curP1Len != kLongMatch) {
+          // finished by pass 1: keep its result; it is also the carry for the next target
+          bestLen = curP1Len;
+          bestDist = curP1Dist;
+          done = true;
+        }
+        for (uint32_t k = 0; !done && k < niv; k++)
           if (p >= iv[k].lo && p < iv[k].hi) {
             // shortcut interval: the reference copies the predecessor's match, minus one
             isIv = true;
@@ -516,7 +713,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           }
         if (isIv) {
           done = true;
-        } else {
+        } else if (!done) {
           key = src.ld4(p);
           room = (uint32_t)(stopAbs - p);
           lb = p > kWindow ? p - kWindow : 0;
@@ -625,10 +822,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
         needInit = true;
       }
     }
-    if (lane < cnt) {
-      const uint64_t idx = S.s0 + first + lane - matchBase;
-      mlen[idx] = resLen;
-      mdist[idx] = (uint16_t)resDist;
+    if (lane < cnt && pass1Len == kLongMatch) {
+      mlen[myIdx] = resLen;
+      mdist[myIdx] = (uint16_t)resDist;
     }
   }
 }
@@ -996,19 +1192,24 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
 uint32_t find_lds_bytes() { return 65536 + 16; }
 
 void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
-                 const uint32_t* ivCount, const uint2* elem, const uint32_t* rank, uint32_t maxChain, uint32_t* mlen,
-                 uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
+                 const uint32_t* ivCount, const uint2* elem, const uint2* compact, const uint32_t* rank, uint32_t maxChain,
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
 {
   if (!nsegs) return;
   if (ldsWindow) {
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)k_find<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
+      hipFuncSetAttribute((const void*)k_find_sorted<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       attr = true;
     }
+    hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
+                       compact, maxChain, mlen, mdist, matchBase);
     hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
                        elem, rank, maxChain, mlen, mdist, matchBase);
   } else {
+    hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
+                       maxChain, mlen, mdist, matchBase);
     hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, elem, rank,
                        maxChain, mlen, mdist, matchBase);
   }
