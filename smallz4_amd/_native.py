@@ -9,7 +9,8 @@ from __future__ import annotations
 import ctypes
 import os
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libsmallz4_amd.so")
+LIB_PATH = os.environ.get("SMALLZ4_AMD_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib",
+                                                               "libsmallz4_amd.so")
 
 SZ4_OK = 0
 SZ4_HEADER_SMALLZ4 = 0

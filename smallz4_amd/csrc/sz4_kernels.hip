@@ -17,6 +17,10 @@
 
 #include "sz4_internal.h"
 
+#ifndef SZ4_DIAG
+#define SZ4_DIAG 0  // diagnostic timing builds only (wrong output): 1 = no parse reductions, 2 = no parse chain
+#endif
+
 namespace sz4 {
 
 // ------------------------------------------------------------------------------------------------
@@ -80,6 +84,18 @@ constexpr int kQuadSwap2 = 0x4E;      // quad_perm [2,3,0,1]
 constexpr int kRowHalfMirror = 0x141;
 constexpr int kRowMirror = 0x140;
 constexpr int kRowShr = 0x110;        // + n
+constexpr int kWaveShr1 = 0x138;      // wave_shr:1 (whole 64-lane wavefront)
+constexpr int kRowBcast15 = 0x142;    // lane 15 of each row -> the next row (rows in row_mask)
+constexpr int kRowBcast31 = 0x143;    // lane 31 -> rows 2 and 3 (rows in row_mask)
+
+// DPP move restricted to the rows of kRowMask; other rows keep v
+template <int kCtrl>
+__device__ __forceinline__ uint32_t dpp_rows_impl(uint32_t v, int rowMask)
+{
+  return rowMask == 0xA ? (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xA, 0xF, false)
+                        : (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xC, 0xF, false);
+}
+#define dpp_rows(v, ctrl, mask) dpp_rows_impl<ctrl>((v), (mask))
 
 // every lane receives the min / max of its 16-lane row
 __device__ __forceinline__ uint32_t row_min(uint32_t v)
@@ -107,6 +123,16 @@ __device__ __forceinline__ uint32_t row_scan_max(uint32_t v)
   v = max(v, dpp<kRowShr + 8>(v));
   return v;
 }
+// wave-wide min delivered to EVERY lane (no SGPR round trip): rows, then row pairs, then halves
+__device__ __forceinline__ uint32_t wave_min_all(uint32_t v)
+{
+  v = row_min(v);
+  auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = min(a[0], a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return min(b[0], b[1]);
+}
+
 // wave-wide min, result uniform
 __device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
 {
@@ -917,57 +943,141 @@ __global__ __launch_bounds__(64) void k_parse(const uint8_t* __restrict__ in, co
       cost[j] = 0;
     }
     __threadfence_block();
-    uint32_t lits = kTailLiterals;
-    uint32_t costNext = 0;  // cost[i + 1]
-    for (int64_t hi = (int64_t)n - 1 - kTailLiterals; hi >= 0; hi -= 64) {
-      const int64_t lo = hi - 63 > 0 ? hi - 63 : 0;
-      const int64_t iMine = hi - (int64_t)lane;
-      const uint32_t myL = iMine >= lo ? ld_fresh(&L[iMine]) : 0;
-      const uint32_t myD = iMine >= lo ? D[iMine] : 0;
-      uint32_t myBest = 1, myCost = 0;
-      for (int64_t i = hi; i >= lo; i--) {
-        const int k = (int)(hi - i);
-        const uint32_t Lk = rdlane(myL, (uint32_t)k);
-        const uint32_t Dk = rdlane(myD, (uint32_t)k);
-        lits++;
-        uint32_t minCost = costNext + 1;
-        if (lits == 15 || (lits >= 15 + 255 && (lits - 15) % 255 == 0)) minCost++;
-        uint32_t best = 1;
-        if (Lk >= kSameLetter && Dk == 1) {
-          const uint64_t j = (uint64_t)i + Lk;
-          const uint32_t cj = Lk < kRing - 64 ? ring[j & (kRing - 1)]
-                                              : ld_fresh(&cost[j]);
-          best = Lk;
-          minCost = cj + 4 + (Lk - 19) / 255;
-        } else if (Lk >= (uint32_t)kMinMatch) {
-          for (uint32_t b = kMinMatch; b <= Lk; b += 64) {
-            const uint32_t len = b + lane;
-            uint32_t keyv = 0xFFFFFFFFu;
-            if (len <= Lk) {
-              const uint64_t j = (uint64_t)i + len;
-              const uint32_t cj = len < kRing - 64 ? ring[j & (kRing - 1)]
-                                                   : ld_fresh(&cost[j]);
-              const uint32_t tot = cj + len_extra(len);
-              keyv = (tot << 6) | (63u - lane);  // min cost, then longest
+    // cost[j] of the last 64 positions lives in lane (j & 63) of `cbuf` (one lane-select per step);
+    // the LDS ring and the HBM spill are written once per 64 positions.
+    // decision state, uniform but kept in vector registers (no SGPR round trips on the chain)
+    uint32_t litsV = kTailLiterals;
+    uint32_t bumpV = 15;    // literal-run length at which a literal costs one more byte (15, 270, ...)
+    uint32_t costV = 0;     // cost[i + 1]
+    uint32_t cbuf = 0;      // cost[n-5 .. n] = 0 (positions past n are never referenced)
+    const int64_t first = (int64_t)n - 1 - kTailLiterals;
+    uint32_t nextL = first - (int64_t)lane >= 0 ? ld_fresh(&L[first - lane]) : 0u;
+    uint32_t nextD = first - (int64_t)lane >= 0 ? (uint32_t)D[first - lane] : 0u;
+
+
+    for (int64_t hi = first; hi >= 0; hi -= 64) {
+      const int32_t lo = hi - 63 > 0 ? (int32_t)(hi - 63) : 0;
+      const int32_t hi32 = (int32_t)hi;
+      // opaque copies: the loop below must not wait for the prefetch issued right after
+      uint32_t myL, myD;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(myL) : "v"(nextL));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(myD) : "v"(nextD));
+      const int64_t iN = hi - 64 - (int64_t)lane;
+      nextL = (hi >= 64 && iN >= 0) ? ld_fresh(&L[iN]) : 0u;  // prefetch the next chunk
+      nextD = (hi >= 64 && iN >= 0) ? (uint32_t)D[iN] : 0u;
+      uint32_t myBest = 1;
+      // Four positions per trip: the candidates of q (lengths >= 4) only read cost[q+4 ..], so
+      // at the start of the trip i0 the minima of i0, i0-1, i0-2, i0-3 are all computable.  Their
+      // four wavefront reductions are independent and interleave; the scalar decisions follow.
+      for (uint32_t t = 0; t < 64; t += 4) {
+        const int32_t i0 = hi32 - (int32_t)t;
+        if (i0 < lo) break;
+        uint32_t Lr[4], Dr[4], kv[4];
+        bool slow = i0 - 3 < lo;  // partial batch at the block start
+        // cbuf lane -> match length for q = i0 - r: ((lane - q - 1) & 63) + 1 in 1..64
+        const uint32_t dl = lane - (uint32_t)i0 - 1u;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          Lr[r] = i0 - r >= lo ? rdlane(myL, t + r) : 0u;
+          Dr[r] = i0 - r >= lo ? rdlane(myD, t + r) : 0u;
+          slow |= Lr[r] > 64u;  // lengths beyond the register window (includes same-letter runs)
+          const uint32_t len = ((dl + (uint32_t)r) & 63u) + 1u;
+          const uint32_t top = Lr[r] < 64 ? Lr[r] : 64u;
+          // key = (cost + 3 [+1 from length 19]) << 6 | (64 - len): minimum = cheapest, then longest
+          const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
+          kv[r] = (len - 4u <= top - 4u && top >= 4u) ? key : 0xFFFFFFFFu;
+        }
+#if SZ4_DIAG == 1
+        // diagnostic build: no candidate reductions
+#else
+#pragma unroll
+        for (int r = 0; r < 4; r++) kv[r] = wave_min_all(kv[r]);
+#endif
+#if SZ4_DIAG == 2
+        if (false) {  // diagnostic build: no decision chain
+#else
+        if (!slow) {
+#endif
+          // the decision chain, entirely in (uniform) vector registers and branch-free
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const uint32_t i = (uint32_t)(i0 - r);
+            litsV++;
+            const bool bump = litsV == bumpV;
+            bumpV = bump ? bumpV + 255u : bumpV;
+            const uint32_t lit = costV + 1u + (bump ? 1u : 0u);
+            const uint32_t mc = kv[r] >> 6;
+            const bool use = kv[r] != 0xFFFFFFFFu && mc <= lit;  // ties go to the match, and the longer one
+            const uint32_t minCost = use ? mc : lit;
+            const uint32_t best = use ? 64u - (kv[r] & 63u) : 1u;
+            litsV = use ? 0u : litsV;
+            bumpV = use ? 15u : bumpV;
+            costV = minCost;
+            cbuf = lane == (i & 63u) ? minCost : cbuf;
+            myBest = lane == t + (uint32_t)r ? best : myBest;
+          }
+        } else {
+          uint32_t lits = rdlane(litsV, 0), litBump = rdlane(bumpV, 0), costNext = rdlane(costV, 0);
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int32_t i = i0 - r;
+            if (i < lo) break;
+            const uint32_t Lk = Lr[r], Dk = Dr[r];
+            lits++;
+            uint32_t minCost = costNext + 1;
+            if (lits == litBump) {
+              minCost++;
+              litBump += 255;
             }
-            const uint32_t kmin = wave_min_fast(keyv);
-            const uint32_t cmin = kmin >> 6;
-            if (kmin != 0xFFFFFFFFu && cmin <= minCost) {
-              minCost = cmin;
-              best = b + (63u - (kmin & 63u));
+            uint32_t best = 1;
+            if (Lk >= (uint32_t)kMinMatch) {
+              if (Lk >= kSameLetter && Dk == 1) {
+                best = Lk;
+                minCost = ld_fresh(&cost[(uint64_t)i + Lk]) + 4 + (Lk - 19) / 255;  // far back: spilled
+              } else {
+                const uint32_t kmin = rdlane(kv[r], 0);
+                if ((kmin >> 6) <= minCost) {
+                  minCost = kmin >> 6;
+                  best = 64u - (kmin & 63u);
+                }
+                // lengths beyond 64: LDS ring (flushed every 64 positions), then the HBM spill
+                for (uint32_t b = 65; b <= Lk; b += 64) {
+                  const uint32_t ln = b + lane;
+                  uint32_t k2 = 0xFFFFFFFFu;
+                  if (ln <= Lk) {
+                    const uint64_t j = (uint64_t)i + ln;
+                    const uint32_t cj = ln < kRing - 64 ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
+                    k2 = ((cj + len_extra(ln)) << 6) | (63u - lane);
+                  }
+                  const uint32_t km = wave_min_fast(k2);
+                  if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
+                    minCost = km >> 6;
+                    best = b + (63u - (km & 63u));
+                  }
+                }
+              }
+            }
+            cbuf = lane == ((uint32_t)i & 63u) ? minCost : cbuf;
+            myBest = lane == t + (uint32_t)r ? best : myBest;
+            costNext = minCost;
+            if (best != 1) {
+              lits = 0;
+              litBump = 15;
             }
           }
+          litsV = lits;
+          bumpV = litBump;
+          costV = costNext;
         }
-        if (lane == 0) ring[(uint64_t)i & (kRing - 1)] = minCost;
-        costNext = minCost;
-        if (lane == (uint32_t)k) { myBest = best; myCost = minCost; }
-        if (best != 1) lits = 0;
       }
-      if (iMine >= lo) {
-        L[iMine] = myBest;
-        cost[iMine] = myCost;
+      // flush: this chunk's chosen lengths, and its costs to the ring and the HBM spill
+      const int64_t iMine = hi - (int64_t)lane;
+      if (iMine >= lo) L[iMine] = myBest;
+      const int64_t jl = lo + (int64_t)((lane - (uint32_t)lo) & 63u);  // position held by this lane
+      if (jl <= hi) {
+        ring[(uint64_t)jl & (kRing - 1)] = cbuf;
+        cost[jl] = cbuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
       }
-      __threadfence_block();
     }
   }
 
