@@ -286,14 +286,25 @@ __global__ __launch_bounds__(256) void k_runs(const uint8_t* __restrict__ in, co
 }
 
 // ================================================================================================
-// k_sort: one 1024-thread workgroup per segment.  Sorts the inserted positions of the window
-// [w0, s1) by (key, position) with a stable LSD radix sort over the four key bytes.  After the
-// sort, the candidates of target p are the entries just below p's slot with the same key --
-// exactly the reference's previousExact chain of p, nearest first.
-// Elements are (key, position - w0) pairs in two ping-pong buffers.
+// k_sort: one 1024-thread workgroup per segment.  Groups the inserted positions of the window
+// [w0, s1) by their four key bytes, positions ascending inside a group: one stable LSD counting
+// sort over a 16-bit hash of the key (two 8-bit passes) on packed 32-bit elements
+// (hash << posBits | position - w0).  Different keys that share a hash land in the same group;
+// the searches compare the four key bytes themselves, so the candidate sets stay exact.  After
+// the sort, the candidates of target p are the same-key entries just below p's slot -- the
+// reference's previousExact chain of p, nearest first.
+// Outputs (in bufB, which the sort no longer needs): per slot the window position and the slot
+// where its hash group starts (u16 each when the window fits 16 bits, u32 otherwise); per target
+// its slot.
 // ================================================================================================
 constexpr int kSortThreads = 1024;
 constexpr int kSortWaves = kSortThreads / 64;
+
+__device__ __forceinline__ uint32_t pos_bits(uint32_t W) { return W <= 65536u ? 16u : 17u; }
+__device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
+{
+  return (key * 2654435761u) >> posBits;  // top (32 - posBits) bits of a multiplicative hash
+}
 
 __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
@@ -304,6 +315,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
   __shared__ uint32_t wsum[4];
   __shared__ uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
   __shared__ uint32_t nEx;
+  __shared__ uint32_t s_scan[kSortThreads];
 
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
@@ -329,12 +341,14 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
   uint64_t excluded = 0;
   for (uint32_t j = 0; j < ne; j++) excluded += exHi[j] - exLo[j];
 
-  uint2* src = bufA + S.elemOff;
-  uint2* dst = bufB + S.elemOff;
+  uint32_t* src = reinterpret_cast<uint32_t*>(bufA + S.elemOff);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   const uint32_t W = (uint32_t)(S.s1 - S.w0);
   const uint32_t E = W - (uint32_t)excluded;
+  const uint32_t pb = pos_bits(W);
+  const uint32_t posMask = (1u << pb) - 1u;
 
-  // 1. elements in position order (intervals compacted out)
+  // 1. packed elements in position order (intervals compacted out)
   for (uint32_t r = tid; r < W; r += kSortThreads) {
     const uint64_t q = S.w0 + r;
     uint32_t idx = r;
@@ -343,19 +357,19 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
       if (q >= exHi[j]) idx -= (uint32_t)(exHi[j] - exLo[j]);
       else if (q >= exLo[j]) skip = true;
     }
-    if (!skip) src[idx] = make_uint2(gload4(in, q), r);
+    if (!skip) src[idx] = (key_hash(gload4(in, q), pb) << pb) | r;
   }
   __syncthreads();
 
-  // 2. four stable counting passes, least significant key byte first
+  // 2. two stable counting passes over the hash bits (low byte first)
   const uint32_t chunk = (((E + kSortWaves - 1) / kSortWaves) + 63) & ~63u;
   const uint32_t b0 = wave * chunk < E ? wave * chunk : E;
   const uint32_t b1 = b0 + chunk < E ? b0 + chunk : E;
-  for (int pass = 0; pass < 4; pass++) {
-    const uint32_t sh = pass * 8;
+  for (int pass = 0; pass < 2; pass++) {
+    const uint32_t sh = pb + 8u * pass;
     for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&hist[wave][(src[i].x >> sh) & 255], 1u);
+    for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&hist[wave][(src[i] >> sh) & 255u], 1u);
     __syncthreads();
     uint32_t total = 0;
     if (tid < 256) {
@@ -378,8 +392,8 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
     for (uint32_t base = b0; base < b1; base += 64) {
       const uint32_t i = base + lane;
       const bool valid = i < b1;
-      const uint2 e = valid ? src[i] : make_uint2(0u, 0u);
-      const uint32_t d = (e.x >> sh) & 255;
+      const uint32_t e = valid ? src[i] : 0u;
+      const uint32_t d = (e >> sh) & 255u;
       uint64_t peers = __ballot(valid);
 #pragma unroll
       for (int b = 0; b < 8; b++) {
@@ -394,48 +408,46 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
       }
     }
     __syncthreads();
-    uint2* t = src;
+    uint32_t* t = src;
     src = dst;
     dst = t;
   }
-  // after four passes the sorted elements are back in bufA; bufB is free and receives the
-  // compact per-slot arrays the sorted-order search reads: window position and the slot where its
-  // key group starts (u16 each when the window fits 16 bits, u32 otherwise)
-  // 3. group starts by a workgroup max-scan over contiguous slot ranges; slot of every target
-  const uint32_t per = (E + kSortThreads - 1) / kSortThreads;
-  const uint32_t r0 = tid * per < E ? tid * per : E;
-  const uint32_t r1 = r0 + per < E ? r0 + per : E;
-  uint32_t localStart = 0;  // last group start inside [r0, r1), +1 (0 = none)
-  for (uint32_t s = r0; s < r1; s++)
-    if (s == 0 || src[s].x != src[s - 1].x) localStart = s + 1;
-  __shared__ uint32_t s_scan[kSortThreads];
-  s_scan[tid] = localStart;
-  __syncthreads();
-  for (uint32_t d = 1; d < kSortThreads; d <<= 1) {
-    const uint32_t v = tid >= d ? s_scan[tid - d] : 0u;
-    __syncthreads();
-    if (v > s_scan[tid]) s_scan[tid] = v;
-    __syncthreads();
-  }
-  uint32_t gs = tid ? s_scan[tid - 1] : 0u;  // inclusive max of earlier threads, +1
-  gs = gs ? gs - 1 : 0;
+  // two passes: sorted elements are back in bufA; bufB receives the per-slot arrays
+  // 3. hash-group starts: tiles of 1024 consecutive slots, inclusive max-scan of (start slot + 1)
+  //    carried across tiles; every access coalesced; slot of every target
   const bool small = W <= 65536u;  // == compact_small(S)
   uint16_t* pos16 = reinterpret_cast<uint16_t*>(bufB + S.elemOff);
   uint16_t* gs16 = pos16 + E;
   uint32_t* pos32 = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   uint32_t* gs32 = pos32 + E;
-  for (uint32_t s = r0; s < r1; s++) {
-    const uint2 e = src[s];
-    if (s == 0 || e.x != src[s - 1].x) gs = s;
-    if (small) {
-      pos16[s] = (uint16_t)e.y;
-      gs16[s] = (uint16_t)gs;
-    } else {
-      pos32[s] = e.y;
-      gs32[s] = gs;
+  uint32_t carry = 0;
+  for (uint32_t base = 0; base < E; base += kSortThreads) {
+    const uint32_t s = base + tid;
+    const bool valid = s < E;
+    const uint32_t e = valid ? src[s] : 0u;
+    const bool start = valid && (s == 0 || (e >> pb) != (src[s - 1] >> pb));
+    uint32_t v = wave_incl_scan_max(start ? s + 1 : 0u);
+    if (lane == 63) s_scan[wave] = v;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (uint32_t w = 0; w < wave; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
+    v = v > pre ? v : pre;
+    if (valid) {
+      const uint32_t g = v - 1u;
+      const uint32_t rel = e & posMask;
+      if (small) {
+        pos16[s] = (uint16_t)rel;
+        gs16[s] = (uint16_t)g;
+      } else {
+        pos32[s] = rel;
+        gs32[s] = g;
+      }
+      const uint64_t q = S.w0 + rel;
+      if (q >= S.s0) rank[S.rankOff + (q - S.s0)] = s;
     }
-    const uint64_t q = S.w0 + e.y;
-    if (q >= S.s0) rank[S.rankOff + (q - S.s0)] = s;
+    for (uint32_t w = wave; w < kSortWaves; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
+    carry = pre;
+    __syncthreads();
   }
 }
 
@@ -452,7 +464,7 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
 //  maxChain <  65535: the reference's step limit counts strict improvements ("records") along the
 //      chain; each 64-candidate step resolves its records with a wavefront prefix-max.
 // ================================================================================================
-constexpr int kFindThreads = 512;  // 8 wavefronts; each 16-lane row owns one target at a time
+constexpr int kFindThreads = 1024;  // 16 wavefronts (2 workgroups = 32 per CU with the 64 KiB window)
 
 template <bool kLds>
 struct Bytes;
@@ -494,7 +506,7 @@ __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t 
 
 // ================================================================================================
 // k_find_sorted (pass 1): one lane per target, targets taken in SORTED order.  A lane's
-// candidates are the slots just below its own inside its key group, so the 64 lanes of a
+// candidates are the same-key slots just below its own inside its hash group, so the 64 lanes of a
 // wavefront read neighbouring slots (coalesced) and lanes of one big group loop the same number
 // of times.  Each lane runs the reference's own nearest-first scan (smallz4.h:190-252): phase-1
 // check at the length it must reach, extension, strict improvement, step limit.  The extension is
@@ -604,6 +616,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __r
             const uint32_t need = bestLen + 1 < 4 ? 4 : bestLen + 1;
             if (cp[u] == 0xFFFFFFFFu || c < lb || need > room) {
               run = false;
+            } else if (src.ld4(c) != key) {
+              // same hash, different four bytes: not on the reference's chain
             } else {
               // phase 1: the four bytes ending at `need` decide most candidates, then the rest
               bool same = need <= 4 || src.ld4(p + need - 4) == src.ld4(c + need - 4);
@@ -646,7 +660,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __r
 template <bool kLds>
 __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
-                                                       const uint32_t* __restrict__ ivCount, const uint2* __restrict__ elemAll,
+                                                       const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                        const uint32_t* __restrict__ rankAll, uint32_t maxChain,
                                                        uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                        uint64_t matchBase)
@@ -656,10 +670,24 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63, row = lane >> 4, li = lane & 15;
-  const uint2* elem = elemAll + S.elemOff;
+  const void* compact = compactAll + S.elemOff;
   const uint32_t* rank = rankAll + S.rankOff;
   const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
   const uint32_t niv = ivCount[S.block];
+  // number of sorted slots (window minus shortcut-interval positions), as in k_sort
+  uint32_t E = (uint32_t)(S.s1 - S.w0);
+  {
+    const uint32_t ids[2] = {B.prev, S.block};
+    for (int t = 0; t < 2; t++) {
+      if (ids[t] == kNoBlock) continue;
+      const Interval* ivb = ivAll + (uint64_t)ids[t] * kMaxIv;
+      for (uint32_t j = 0; j < ivCount[ids[t]]; j++) {
+        const uint64_t lo = ivb[j].lo > S.w0 ? ivb[j].lo : S.w0, hi = ivb[j].hi < S.s1 ? ivb[j].hi : S.s1;
+        if (lo < hi) E -= (uint32_t)(hi - lo);
+      }
+    }
+  }
+  const bool small = compact_small(S);
 
   if (tid == 0) s_next = 0;
   Bytes<kLds> src;
@@ -708,7 +736,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     uint32_t j = 0;  // target index inside the row
     bool needInit = true, done = false, isIv = false;
     uint64_t p = 0, lb = 0;
-    uint32_t key = 0, room = 0, bestLen = 0, bestDist = 0, steps = 0;
+    uint32_t key = 0, room = 0, bestLen = 0, bestDist = 0, steps = 0, gsCur = 0;
     int64_t slot = 0;
     uint32_t carryLen = 0, carryDist = 0;
     uint32_t resLen = pass1Len, resDist = pass1Dist;  // lane rowBase+t holds the result of target first+rowBase+t
@@ -745,6 +773,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           lb = p > kWindow ? p - kWindow : 0;
           if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
           slot = (int64_t)rCur - 1;
+          gsCur = slot_gs(compact, small, E, rCur);
           if (unlimited) {
             bestLen = 0;
             bestDist = 0;
@@ -765,16 +794,16 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
       }
       // one step: 16 candidates of the row's key group, nearest first
       const bool act = live && !done;
-      bool valid = false;
+      bool valid = false, exhausted = true;
       uint32_t got = 0, dist = 0;
       if (act) {
         const int64_t sl = slot - (int64_t)li;
-        if (sl >= 0) {
-          const uint2 e = elem[sl];
-          const uint64_t c = S.w0 + e.y;
-          valid = e.x == key && c >= lb;
+        if (sl >= (int64_t)gsCur) {
+          const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)sl);
+          exhausted = c < lb;  // positions descend inside the group: everything further is older
+          dist = (uint32_t)(p - c);
+          valid = !exhausted && src.ld4(c) == key;  // same hash, same four bytes
           if (valid) {
-            dist = (uint32_t)(p - c);
             if (unlimited) {
               if (dist != bestDist) {
                 const uint32_t need = dist < bestDist ? bestLen : bestLen + 1;
@@ -788,7 +817,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           }
         }
       }
-      const uint32_t rowValid = (uint32_t)(__ballot(valid) >> rowBase) & 0xFFFFu;
+      const uint32_t rowExhausted = (uint32_t)(__ballot(exhausted) >> rowBase) & 0xFFFFu;
       if (unlimited) {
         // longest, then nearest (lower lane = nearer candidate)
         const uint32_t top = row_max(got ? (got << 4) | (15u - li) : 0u);
@@ -802,7 +831,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
               bestDist = wdist;
             }
           }
-          if (rowValid != 0xFFFFu) done = true;                           // key group / window exhausted
+          if (rowExhausted != 0u) done = true;                           // key group / window exhausted
           else if (bestLen >= room && farDist >= bestDist) done = true;   // nothing left can win
           slot -= 16;
         }
@@ -832,7 +861,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
             if (nrec >= steps) done = true;
             else steps -= nrec;
           }
-          if (rowValid != 0xFFFFu || bestLen >= room) done = true;
+          if (rowExhausted != 0u || bestLen >= room) done = true;
           slot -= 16;
         }
       }
@@ -1316,11 +1345,11 @@ void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
     hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
                        compact, maxChain, mlen, mdist, matchBase);
     hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                       elem, rank, maxChain, mlen, mdist, matchBase);
+                       compact, rank, maxChain, mlen, mdist, matchBase);
   } else {
     hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
                        maxChain, mlen, mdist, matchBase);
-    hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, elem, rank,
+    hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
                        maxChain, mlen, mdist, matchBase);
   }
 }
