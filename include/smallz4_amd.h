@@ -93,7 +93,8 @@ void sz4_set_timing(sz4_ctx* ctx, int on);
 /* Diagnostics: stop the pipeline after stage `stop_after` (0 = run everything,
  * 3 = after the match search, 4 = after the parse) on subsequent calls, and copy
  * the per-position match arrays of the last call (length u32, distance u16, one
- * entry per input byte) to host memory.  Used by the intermediate parity tests. */
+ * entry per input byte) to host memory.  After stage 4 at levels > 3 the lengths
+ * are the parse's choices (1 = literal).  Used by the intermediate parity tests. */
 void sz4_debug_stop_after(sz4_ctx* ctx, int stop_after);
 int sz4_debug_matches(sz4_ctx* ctx, uint32_t* len, uint16_t* dist, uint64_t n);
 

@@ -85,11 +85,14 @@ struct sz4_ctx {
   float stageMs[5] = {};
   uint32_t lastBlocks = 0;
   int stopAfter = 0;
+  uint32_t lastChain = 0;
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
+  DevBuf dpSegs, sel, reach, segState;
 
   std::vector<Block> hBlocks;
   std::vector<Segment> hSegs;
+  std::vector<DpSeg> hDp;
   uint64_t elemTotal = 0, rankTotal = 0, tokTotal = 0;
   bool ldsWindow = false;
   // plan cache for sz4_compress_blocks_device
@@ -140,6 +143,22 @@ void finish_plan(sz4_ctx* c)
   c->hSegs.clear();
   c->elemTotal = c->rankTotal = 0;
   for (uint32_t b = 0; b < c->hBlocks.size(); b++) add_segments(c, b);
+  // parse segments: positions [0, n - 6] of every block longer than 12 bytes, top segment first
+  c->hDp.clear();
+  for (uint32_t b = 0; b < c->hBlocks.size(); b++) {
+    Block& B = c->hBlocks[b];
+    const uint64_t n = B.end - B.start;
+    B.dpFirst = (uint32_t)c->hDp.size();
+    B.dpCount = 0;
+    if (n <= (uint64_t)kTailNoMatch) continue;
+    const uint64_t top = n - 1 - kTailLiterals;
+    for (uint64_t hi = top, k = 0;; hi -= kDpSeg, k++) {
+      const uint64_t lo = hi + 1 >= kDpSeg ? hi + 1 - kDpSeg : 0;
+      c->hDp.push_back(DpSeg{b, (uint32_t)k, (uint32_t)lo, (uint32_t)hi});
+      B.dpCount++;
+      if (lo == 0) break;
+    }
+  }
   c->ldsWindow = true;
   for (const Segment& S : c->hSegs) {
     const Block& B = c->hBlocks[S.block];
@@ -165,7 +184,11 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->ntok.reserve(nb * 4 + 64)) ||
       (e = c->blockBytes.reserve(nb * 4 + 64)) ||
       (e = c->offsets.reserve((nb + 1) * 8 + 64)) ||
-      (e = c->status.reserve(64)))
+      (e = c->status.reserve(64)) ||
+      (e = c->dpSegs.reserve(c->hDp.size() * sizeof(DpSeg) + 64)) ||
+      (e = c->sel.reserve(stagedBytes * 4 + 64)) ||
+      (e = c->reach.reserve(stagedBytes * 4 + 64)) ||
+      (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)))
     return c->fail(SZ4_E_NOMEM, "device allocation", e);
   return SZ4_OK;
 }
@@ -181,9 +204,11 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
 {
   const uint32_t nb = (uint32_t)c->hBlocks.size();
   const uint8_t* in = c->staged.as<uint8_t>();
+  c->lastChain = maxChain;
   hipError_t e;
   if ((e = hipMemcpyAsync(c->blocks.p, c->hBlocks.data(), nb * sizeof(Block), hipMemcpyHostToDevice, s)) ||
       (e = hipMemcpyAsync(c->segs.p, c->hSegs.data(), c->hSegs.size() * sizeof(Segment), hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(c->dpSegs.p, c->hDp.data(), c->hDp.size() * sizeof(DpSeg), hipMemcpyHostToDevice, s)) ||
       (e = hipMemsetAsync(c->status.p, 0, 4, s)))
     return c->fail(SZ4_E_DEVICE, "upload plan", e);
   const uint32_t ns = (uint32_t)c->hSegs.size();
@@ -206,11 +231,14 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   }
   mark(c, 3, s);
   if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
-  launch_parse(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(),
-               c->status.as<int>(), s);
+  launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
+               c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
+               c->segState.as<uint4>(), c->status.as<int>(), s);
   mark(c, 4, s);
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
-  launch_emit(in, dB, nb, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->tokens.as<Token>(),
+  // optimal levels tokenize the parse's choices, greedy/lazy levels the (skip-filtered) matches
+  const uint32_t* chosen = maxChain > (uint32_t)kGreedyMax ? c->sel.as<uint32_t>() : c->mlen.as<uint32_t>();
+  launch_emit(in, dB, nb, maxChain, chosen, c->mdist.as<uint16_t>(), 0, c->tokens.as<Token>(),
               c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen, s);
   mark(c, 5, s);
   if ((e = hipGetLastError())) return c->fail(SZ4_E_DEVICE, "kernel launch", e);
@@ -263,7 +291,8 @@ void sz4_destroy(sz4_ctx* c)
   if (!c) return;
   hipSetDevice(c->device);
   for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
-                    &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status})
+                    &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
+                    &c->sel, &c->reach, &c->segState})
     b->release();
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -445,7 +474,9 @@ int sz4_debug_matches(sz4_ctx* c, uint32_t* len, uint16_t* dist, uint64_t n)
 {
   if (!c || !len || !dist) return SZ4_E_ARG;
   if (n * 4 > c->mlen.cap || n * 2 > c->mdist.cap) return SZ4_E_ARG;
-  if (hipMemcpy(len, c->mlen.p, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+  // after the parse at optimal levels the lengths are the parse's choices
+  const DevBuf& lens = c->stopAfter == 4 && c->lastChain > (uint32_t)kGreedyMax ? c->sel : c->mlen;
+  if (hipMemcpy(len, lens.p, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(dist, c->mdist.p, n * 2, hipMemcpyDeviceToHost) != hipSuccess)
     return SZ4_E_DEVICE;
   return SZ4_OK;

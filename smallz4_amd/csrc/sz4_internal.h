@@ -27,6 +27,8 @@ struct Block {
   uint64_t tokOff;         // first Token slot of this block (capacity (end-start)/2 + 4)
   uint32_t prev;           // index of the previous block of the same stream, or kNoBlock
   uint32_t flags;          // kBlk* below
+  uint32_t dpFirst;        // first DpSeg of this block (top segment first)
+  uint32_t dpCount;        // number of DpSegs (0 when the block is too short to parse)
 };
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kBlkLegacy = 1;         // always emitted compressed (legacy frame)
@@ -50,6 +52,17 @@ struct Interval {
 // block b owns iv[b * kMaxIv .. b * kMaxIv + ivCount[b])
 constexpr uint32_t kMaxIv = 136;  // > 8 MiB / 65300
 
+// the optimal parse of one block runs as independent segments of kDpSeg positions (top segment
+// first, k = 0): every segment is parsed at once from a guessed boundary, then k_dp_fix walks the
+// boundaries top-down and re-parses each segment until it agrees with the speculative parse.
+struct DpSeg {
+  uint32_t block;
+  uint32_t k;              // 0 = the segment holding the block's last parsed position
+  uint32_t lo, hi;         // block-relative positions [lo, hi], parsed from hi down
+};
+constexpr uint32_t kDpSeg = 16384;
+constexpr uint32_t kMaxDpSegs = 512;  // 8 MiB legacy block / kDpSeg
+
 // one LZ4 sequence: literal run [litFrom, litFrom+lits) (block-relative) then a match
 struct Token {
   uint32_t litFrom, lits, mlen, dist;  // dist: low 16 bits; kTokLast marks the final literals-only token
@@ -67,9 +80,10 @@ void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
                  const Interval* iv, const uint32_t* ivCount, const uint2* elem, const uint2* compact,
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  bool ldsWindow, hipStream_t s);
-void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const Interval* iv,
+void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
-                  uint64_t matchBase, uint32_t* cost, int* status, hipStream_t s);
+                  uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, int* status,
+                  hipStream_t s);
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
                  const uint16_t* mdist, uint64_t matchBase, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
                  uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s);

@@ -885,231 +885,371 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
 }
 
 // ================================================================================================
-// k_parse: one wavefront per block.
-//   1. greedy/lazy levels: the reference's skip scan decides which searched positions it keeps
-//      (smallz4.h:726-744);
-//   2. levels > 3: backward optimal parse (estimateCosts, smallz4.h:376-472).  Costs of the last
-//      kRing positions live in an LDS ring, older ones in HBM; per position the wavefront scores
-//      64 match lengths per step and reduces (cost, -length) with a wave minimum;
+// The parse, after the matches are known.
+//   k_prep    one wavefront per block: clears the positions the reference never searched and, at
+//             greedy/lazy levels, replays the reference's skip scan (smallz4.h:726-744);
+//   k_dp_spec one wavefront per DpSeg: the backward optimal parse (estimateCosts,
+//             smallz4.h:376-472) of kDpSeg positions.  The top segment of a block starts from the
+//             block end exactly; every other segment starts from a guessed boundary (costs 0 above
+//             it).  Also writes reach[i] = max(q + len[q]) over the segment's positions q < i.
+//   k_dp_fix  one wavefront per block: walks the segment boundaries top-down.  Segment k is parsed
+//             again from the true state above it until the exact and the speculative parse agree:
+//             both choose a match at i (so the literal counters agree) and exact - speculative
+//             costs are one constant over every position [i, reach[i]] the rest of the segment can
+//             reference.  Choices depend on cost differences only, so below i the speculative
+//             choices are the exact ones and exact costs are speculative costs + that constant.
+// Costs of recent positions sit in a register window (lane j & 63 holds cost[j]) and an LDS ring;
+// older ones are read back from HBM.
 // ================================================================================================
-constexpr int kRing = 4096;
+constexpr int kRing = 1024;
 
 __device__ __forceinline__ uint32_t len_extra(uint32_t len)
 {
   return len < 19 ? 3u : 4u + (len - 19) / 255;
 }
 
-__global__ __launch_bounds__(64) void k_parse(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
-                                              const Interval* __restrict__ ivAll, const uint32_t* __restrict__ ivCount,
-                                              uint32_t maxChain, uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
-                                              uint64_t matchBase, uint32_t* __restrict__ costAll, int* __restrict__ status)
+__global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, const uint32_t* __restrict__ ivCount,
+                                             uint32_t maxChain, uint32_t* __restrict__ mlen, uint64_t matchBase,
+                                             uint32_t* __restrict__ sel, int* __restrict__ status)
 {
-  __shared__ uint32_t ring[kRing];
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const uint64_t n = B.end - B.start;
   uint32_t* L = mlen + (B.start - matchBase);
-  const uint16_t* D = mdist + (B.start - matchBase);
-  uint32_t* cost = costAll + (B.start - matchBase) + blockIdx.x;  // n + 1 entries per block
-  const Interval* iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
-  const uint32_t niv = ivCount[blockIdx.x];
-  const bool stored = maxChain == 0;
-  const bool legacy = (B.flags & kBlkLegacy) != 0;
+  uint32_t* S = sel + (B.start - matchBase);
+  if (maxChain == 0) return;
   const uint64_t lastSearch = n >= (uint64_t)kTailNoMatch ? n - kTailNoMatch : 0;  // inclusive, relative
 
   // positions the reference never searched keep length 0 (it leaves them default-constructed)
-  if (!stored && n >= (uint64_t)kTailNoMatch) {
-    for (uint64_t i = lastSearch + 1 + lane; i < n; i += 64) L[i] = 0;
-  } else if (!stored) {
-    for (uint64_t i = lane; i < n; i += 64) L[i] = 0;
+  for (uint64_t i = (n >= (uint64_t)kTailNoMatch ? lastSearch + 1 : 0) + lane; i < n; i += 64) L[i] = 0;
+  if (maxChain > (uint32_t)kGreedyMax) {
+    // the parse writes positions [0, n - 6]; the block ends with literals
+    const uint64_t from = n > (uint64_t)kTailNoMatch ? n - kTailLiterals : 0;
+    for (uint64_t i = from + lane; i < n; i += 64) S[i] = 0;
   }
+  if (maxChain > (uint32_t)kLazyMax || n < (uint64_t)kTailNoMatch) return;
+  if (ivCount[blockIdx.x] && lane == 0) atomicOr(status, 1);  // shortcut interplay with skipping: not on this path
 
-  // ---- 1. greedy / lazy skip scan ---------------------------------------------------------------
-  if (!stored && maxChain <= (uint32_t)kLazyMax && n >= (uint64_t)kTailNoMatch) {
-    if (niv) {
-      if (lane == 0) atomicOr(status, 1);  // shortcut interplay with skipping: not on this path
-    }
-    // one lane replays the reference's bookkeeping over an LDS copy of each 64-position chunk
-    __shared__ uint32_t chunkL[64];
-    uint64_t skip = 0;
-    bool lazyEval = false;
-    for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
-      const uint64_t i = c0 + lane;
-      const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
-      chunkL[lane] = i <= lastSearch ? ld_fresh(&L[i]) : 0u;
-      __syncthreads();
-      if (lane == 0) {
-        for (uint32_t k = 0; k < cnt; k++) {
-          const uint32_t lk = chunkL[k];
-          // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
-          if (lk >= (uint32_t)kMinMatch) {
-            bool search = true;
-            if (skip > 0) {
-              skip--;
-              search = lazyEval;  // a pending lazy evaluation searches one more position
-              lazyEval = false;
-            }
-            if (search) {
-              lazyEval = (skip == 0);
-              skip = lk;
-            } else {
-              chunkL[k] = 0;  // never searched by the reference
-            }
+  // one lane replays the reference's bookkeeping over an LDS copy of each 64-position chunk
+  __shared__ uint32_t chunkL[64];
+  uint64_t skip = 0;
+  bool lazyEval = false;
+  for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
+    const uint64_t i = c0 + lane;
+    const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
+    chunkL[lane] = i <= lastSearch ? L[i] : 0u;
+    __syncthreads();
+    if (lane == 0) {
+      for (uint32_t k = 0; k < cnt; k++) {
+        const uint32_t lk = chunkL[k];
+        // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
+        if (lk >= (uint32_t)kMinMatch) {
+          bool search = true;
+          if (skip > 0) {
+            skip--;
+            search = lazyEval;  // a pending lazy evaluation searches one more position
+            lazyEval = false;
+          }
+          if (search) {
+            lazyEval = (skip == 0);
+            skip = lk;
+          } else {
+            chunkL[k] = 0;  // never searched by the reference
           }
         }
       }
-      __syncthreads();
-      if (i <= lastSearch) L[i] = chunkL[lane];
-      __syncthreads();
     }
-    __threadfence_block();
+    __syncthreads();
+    if (i <= lastSearch) L[i] = chunkL[lane];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
+                                                const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                                uint64_t matchBase, uint32_t* __restrict__ costAll,
+                                                uint32_t* __restrict__ sel, uint32_t* __restrict__ reach,
+                                                uint4* __restrict__ segState)
+{
+  __shared__ uint32_t ring[kRing];
+  const DpSeg G = dpSegs[blockIdx.x];
+  const Block B = blocks[G.block];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t base = B.start - matchBase;
+  const uint32_t* L = mlen + base;
+  const uint16_t* D = mdist + base;
+  uint32_t* cost = costAll + base;
+  uint32_t* S = sel + base;
+  const int32_t segLo = (int32_t)G.lo, segHi = (int32_t)G.hi;
+
+  // reach[i] = max over q in [lo, i) of q + len[q]: the highest cost a position below i reads
+  if (G.k > 0) {
+    uint32_t* R = reach + base;
+    uint32_t carry = 0;
+    for (int32_t c0 = segLo; c0 <= segHi; c0 += 64) {
+      const int32_t q = c0 + (int32_t)lane;
+      const uint32_t v = q <= segHi ? (uint32_t)q + L[q] : 0u;
+      const uint32_t incl = wave_incl_scan_max(v);
+      uint32_t excl = __shfl_up(incl, 1, 64);
+      excl = lane == 0 ? carry : (excl > carry ? excl : carry);
+      if (q <= segHi) R[q] = excl;
+      const uint32_t top = rdlane(incl, 63);
+      carry = top > carry ? top : carry;
+    }
   }
 
-  // ---- 2. backward optimal parse ---------------------------------------------------------------
-  if (!stored && n > (uint64_t)kTailNoMatch && maxChain > (uint32_t)kGreedyMax) {
-    for (uint64_t j = n - kTailLiterals + lane; j <= n; j += 64) {
-      ring[j & (kRing - 1)] = 0;
-      cost[j] = 0;
-    }
-    __threadfence_block();
-    // cost[j] of the last 64 positions lives in lane (j & 63) of `cbuf` (one lane-select per step);
-    // the LDS ring and the HBM spill are written once per 64 positions.
-    // decision state, uniform but kept in vector registers (no SGPR round trips on the chain)
-    uint32_t litsV = kTailLiterals;
-    uint32_t bumpV = 15;    // literal-run length at which a literal costs one more byte (15, 270, ...)
-    uint32_t costV = 0;     // cost[i + 1]
-    uint32_t cbuf = 0;      // cost[n-5 .. n] = 0 (positions past n are never referenced)
-    const int64_t first = (int64_t)n - 1 - kTailLiterals;
-    uint32_t nextL = first - (int64_t)lane >= 0 ? ld_fresh(&L[first - lane]) : 0u;
-    uint32_t nextD = first - (int64_t)lane >= 0 ? (uint32_t)D[first - lane] : 0u;
+  // decision state, uniform but kept in vector registers (no SGPR round trips on the chain);
+  // the top segment starts exactly (costs past the block end are 0, five trailing literals)
+  uint32_t litsV = G.k == 0 ? (uint32_t)kTailLiterals : 0u;
+  uint32_t bumpV = 15;    // literal-run length at which a literal costs one more byte (15, 270, ...)
+  uint32_t costV = 0;     // cost[i + 1]
+  uint32_t cbuf = 0;      // cost[j] of the 64 positions above i, in lane j & 63
+  uint32_t nextL = segHi - (int32_t)lane >= segLo ? L[segHi - lane] : 0u;
+  uint32_t nextD = segHi - (int32_t)lane >= segLo ? (uint32_t)D[segHi - lane] : 0u;
+  // cost read-back above the register window: above the segment the guess is 0 (exact for k = 0)
+  auto far_cost = [&](int32_t i, uint32_t ln) -> uint32_t {
+    const int32_t j = i + (int32_t)ln;
+    if (j > segHi) return 0u;
+    return ln < (uint32_t)kRing - 64u ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
+  };
 
-
-    for (int64_t hi = first; hi >= 0; hi -= 64) {
-      const int32_t lo = hi - 63 > 0 ? (int32_t)(hi - 63) : 0;
-      const int32_t hi32 = (int32_t)hi;
-      // opaque copies: the loop below must not wait for the prefetch issued right after
-      uint32_t myL, myD;
-      asm volatile("v_mov_b32 %0, %1" : "=v"(myL) : "v"(nextL));
-      asm volatile("v_mov_b32 %0, %1" : "=v"(myD) : "v"(nextD));
-      const int64_t iN = hi - 64 - (int64_t)lane;
-      nextL = (hi >= 64 && iN >= 0) ? ld_fresh(&L[iN]) : 0u;  // prefetch the next chunk
-      nextD = (hi >= 64 && iN >= 0) ? (uint32_t)D[iN] : 0u;
-      uint32_t myBest = 1;
-      // Four positions per trip: the candidates of q (lengths >= 4) only read cost[q+4 ..], so
-      // at the start of the trip i0 the minima of i0, i0-1, i0-2, i0-3 are all computable.  Their
-      // four wavefront reductions are independent and interleave; the scalar decisions follow.
-      for (uint32_t t = 0; t < 64; t += 4) {
-        const int32_t i0 = hi32 - (int32_t)t;
-        if (i0 < lo) break;
-        uint32_t Lr[4], Dr[4], kv[4];
-        bool slow = i0 - 3 < lo;  // partial batch at the block start
-        // cbuf lane -> match length for q = i0 - r: ((lane - q - 1) & 63) + 1 in 1..64
-        const uint32_t dl = lane - (uint32_t)i0 - 1u;
+  for (int32_t hi = segHi; hi >= segLo; hi -= 64) {
+    const int32_t lo = hi - 63 > segLo ? hi - 63 : segLo;
+    // opaque copies: the loop below must not wait for the prefetch issued right after
+    uint32_t myL, myD;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(myL) : "v"(nextL));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(myD) : "v"(nextD));
+    const int32_t iN = hi - 64 - (int32_t)lane;
+    nextL = iN >= segLo ? L[iN] : 0u;  // prefetch the next chunk
+    nextD = iN >= segLo ? (uint32_t)D[iN] : 0u;
+    uint32_t myBest = 1;
+    // Four positions per trip: the candidates of q (lengths >= 4) only read cost[q+4 ..], so
+    // at the start of the trip i0 the minima of i0, i0-1, i0-2, i0-3 are all computable.  Their
+    // four wavefront reductions are independent and interleave; the decisions follow.
+    for (uint32_t t = 0; t < 64; t += 4) {
+      const int32_t i0 = hi - (int32_t)t;
+      if (i0 < lo) break;
+      uint32_t Lr[4], Dr[4], kv[4];
+      bool slow = i0 - 3 < lo;  // partial batch at the segment start
+      // cbuf lane -> match length for q = i0 - r: ((lane - q - 1) & 63) + 1 in 1..64
+      const uint32_t dl = lane - (uint32_t)i0 - 1u;
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        Lr[r] = i0 - r >= lo ? rdlane(myL, t + r) : 0u;
+        Dr[r] = i0 - r >= lo ? rdlane(myD, t + r) : 0u;
+        slow |= Lr[r] > 64u;  // lengths beyond the register window (includes same-letter runs)
+        const uint32_t len = ((dl + (uint32_t)r) & 63u) + 1u;
+        const uint32_t top = Lr[r] < 64 ? Lr[r] : 64u;
+        // key = (cost + 3 [+1 from length 19]) << 6 | (64 - len): minimum = cheapest, then longest
+        const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
+        kv[r] = (len - 4u <= top - 4u && top >= 4u) ? key : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) kv[r] = wave_min_all(kv[r]);
+      if (!slow) {
+        // the decision chain, entirely in (uniform) vector registers and branch-free
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-          Lr[r] = i0 - r >= lo ? rdlane(myL, t + r) : 0u;
-          Dr[r] = i0 - r >= lo ? rdlane(myD, t + r) : 0u;
-          slow |= Lr[r] > 64u;  // lengths beyond the register window (includes same-letter runs)
-          const uint32_t len = ((dl + (uint32_t)r) & 63u) + 1u;
-          const uint32_t top = Lr[r] < 64 ? Lr[r] : 64u;
-          // key = (cost + 3 [+1 from length 19]) << 6 | (64 - len): minimum = cheapest, then longest
-          const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
-          kv[r] = (len - 4u <= top - 4u && top >= 4u) ? key : 0xFFFFFFFFu;
+          const uint32_t i = (uint32_t)(i0 - r);
+          litsV++;
+          const bool bump = litsV == bumpV;
+          bumpV = bump ? bumpV + 255u : bumpV;
+          const uint32_t lit = costV + 1u + (bump ? 1u : 0u);
+          const uint32_t mc = kv[r] >> 6;
+          const bool use = kv[r] != 0xFFFFFFFFu && mc <= lit;  // ties go to the match, and the longer one
+          const uint32_t minCost = use ? mc : lit;
+          const uint32_t best = use ? 64u - (kv[r] & 63u) : 1u;
+          litsV = use ? 0u : litsV;
+          bumpV = use ? 15u : bumpV;
+          costV = minCost;
+          cbuf = lane == (i & 63u) ? minCost : cbuf;
+          myBest = lane == t + (uint32_t)r ? best : myBest;
         }
-#if SZ4_DIAG == 1
-        // diagnostic build: no candidate reductions
-#else
+      } else {
+        uint32_t lits = rdlane(litsV, 0), litBump = rdlane(bumpV, 0), costNext = rdlane(costV, 0);
 #pragma unroll
-        for (int r = 0; r < 4; r++) kv[r] = wave_min_all(kv[r]);
-#endif
-#if SZ4_DIAG == 2
-        if (false) {  // diagnostic build: no decision chain
-#else
-        if (!slow) {
-#endif
-          // the decision chain, entirely in (uniform) vector registers and branch-free
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const uint32_t i = (uint32_t)(i0 - r);
-            litsV++;
-            const bool bump = litsV == bumpV;
-            bumpV = bump ? bumpV + 255u : bumpV;
-            const uint32_t lit = costV + 1u + (bump ? 1u : 0u);
-            const uint32_t mc = kv[r] >> 6;
-            const bool use = kv[r] != 0xFFFFFFFFu && mc <= lit;  // ties go to the match, and the longer one
-            const uint32_t minCost = use ? mc : lit;
-            const uint32_t best = use ? 64u - (kv[r] & 63u) : 1u;
-            litsV = use ? 0u : litsV;
-            bumpV = use ? 15u : bumpV;
-            costV = minCost;
-            cbuf = lane == (i & 63u) ? minCost : cbuf;
-            myBest = lane == t + (uint32_t)r ? best : myBest;
+        for (int r = 0; r < 4; r++) {
+          const int32_t i = i0 - r;
+          if (i < lo) break;
+          const uint32_t Lk = Lr[r], Dk = Dr[r];
+          lits++;
+          uint32_t minCost = costNext + 1;
+          if (lits == litBump) {
+            minCost++;
+            litBump += 255;
           }
-        } else {
-          uint32_t lits = rdlane(litsV, 0), litBump = rdlane(bumpV, 0), costNext = rdlane(costV, 0);
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int32_t i = i0 - r;
-            if (i < lo) break;
-            const uint32_t Lk = Lr[r], Dk = Dr[r];
-            lits++;
-            uint32_t minCost = costNext + 1;
-            if (lits == litBump) {
-              minCost++;
-              litBump += 255;
-            }
-            uint32_t best = 1;
-            if (Lk >= (uint32_t)kMinMatch) {
-              if (Lk >= kSameLetter && Dk == 1) {
-                best = Lk;
-                minCost = ld_fresh(&cost[(uint64_t)i + Lk]) + 4 + (Lk - 19) / 255;  // far back: spilled
-              } else {
-                const uint32_t kmin = rdlane(kv[r], 0);
-                if ((kmin >> 6) <= minCost) {
-                  minCost = kmin >> 6;
-                  best = 64u - (kmin & 63u);
-                }
-                // lengths beyond 64: LDS ring (flushed every 64 positions), then the HBM spill
-                for (uint32_t b = 65; b <= Lk; b += 64) {
-                  const uint32_t ln = b + lane;
-                  uint32_t k2 = 0xFFFFFFFFu;
-                  if (ln <= Lk) {
-                    const uint64_t j = (uint64_t)i + ln;
-                    const uint32_t cj = ln < kRing - 64 ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
-                    k2 = ((cj + len_extra(ln)) << 6) | (63u - lane);
-                  }
-                  const uint32_t km = wave_min_fast(k2);
-                  if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
-                    minCost = km >> 6;
-                    best = b + (63u - (km & 63u));
-                  }
+          uint32_t best = 1;
+          if (Lk >= (uint32_t)kMinMatch) {
+            if (Lk >= kSameLetter && Dk == 1) {
+              best = Lk;
+              const int32_t j = i + (int32_t)Lk;  // far back: spilled
+              minCost = (j > segHi ? 0u : ld_fresh(&cost[j])) + 4 + (Lk - 19) / 255;
+            } else {
+              const uint32_t kmin = rdlane(kv[r], 0);
+              if ((kmin >> 6) <= minCost) {
+                minCost = kmin >> 6;
+                best = 64u - (kmin & 63u);
+              }
+              // lengths beyond 64: LDS ring (flushed every 64 positions), then the HBM spill
+              for (uint32_t b = 65; b <= Lk; b += 64) {
+                const uint32_t ln = b + lane;
+                uint32_t k2 = 0xFFFFFFFFu;
+                if (ln <= Lk) k2 = ((far_cost(i, ln) + len_extra(ln)) << 6) | (63u - lane);
+                const uint32_t km = wave_min_fast(k2);
+                if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
+                  minCost = km >> 6;
+                  best = b + (63u - (km & 63u));
                 }
               }
             }
-            cbuf = lane == ((uint32_t)i & 63u) ? minCost : cbuf;
-            myBest = lane == t + (uint32_t)r ? best : myBest;
-            costNext = minCost;
-            if (best != 1) {
-              lits = 0;
-              litBump = 15;
-            }
           }
-          litsV = lits;
-          bumpV = litBump;
-          costV = costNext;
+          cbuf = lane == ((uint32_t)i & 63u) ? minCost : cbuf;
+          myBest = lane == t + (uint32_t)r ? best : myBest;
+          costNext = minCost;
+          if (best != 1) {
+            lits = 0;
+            litBump = 15;
+          }
         }
-      }
-      // flush: this chunk's chosen lengths, and its costs to the ring and the HBM spill
-      const int64_t iMine = hi - (int64_t)lane;
-      if (iMine >= lo) L[iMine] = myBest;
-      const int64_t jl = lo + (int64_t)((lane - (uint32_t)lo) & 63u);  // position held by this lane
-      if (jl <= hi) {
-        ring[(uint64_t)jl & (kRing - 1)] = cbuf;
-        cost[jl] = cbuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
+        litsV = lits;
+        bumpV = litBump;
+        costV = costNext;
       }
     }
+    // flush: this chunk's choices, and its costs to the ring and the HBM spill
+    const int32_t iMine = hi - (int32_t)lane;
+    if (iMine >= lo) S[iMine] = myBest;
+    const int32_t jl = lo + (int32_t)((lane - (uint32_t)lo) & 63u);  // position held by this lane
+    if (jl <= hi) {
+      ring[jl & (kRing - 1)] = cbuf;
+      cost[jl] = cbuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
+    }
   }
+  if (lane == 0) segState[blockIdx.x] = make_uint4(rdlane(litsV, 0), rdlane(bumpV, 0), 0u, 0u);
+}
 
+__global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
+                                               const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                               uint64_t matchBase, uint32_t* __restrict__ costAll,
+                                               uint32_t* __restrict__ sel, const uint32_t* __restrict__ reach,
+                                               uint4* __restrict__ segState)
+{
+  __shared__ uint32_t ring[kRing];
+  __shared__ uint32_t convTab[kMaxDpSegs];   // positions >= convTab[k] of segment k hold exact costs
+  __shared__ uint32_t deltaTab[kMaxDpSegs];  // below it: exact = stored + deltaTab[k]
+  const Block B = blocks[blockIdx.x];
+  if (B.dpCount <= 1) return;
+  const uint32_t lane = threadIdx.x;
+  const uint64_t base = B.start - matchBase;
+  const uint32_t* L = mlen + base;
+  const uint16_t* D = mdist + base;
+  const uint32_t* R = reach + base;
+  uint32_t* cost = costAll + base;
+  uint32_t* S = sel + base;
+  const uint32_t first = dpSegs[B.dpFirst].hi;  // n - 6: the last parsed position
+  if (lane == 0) {
+    convTab[0] = 0;  // the top segment was parsed exactly
+    deltaTab[0] = 0;
+  }
+  __syncthreads();
+  // exact cost of a position above the segment being repaired (0 past the parsed range)
+  auto exact_above = [&](uint32_t j) -> uint32_t {
+    if (j > first) return 0u;
+    const uint32_t k = (first - j) / kDpSeg;
+    const uint32_t v = ld_fresh(&cost[j]);
+    return j < convTab[k] ? v + deltaTab[k] : v;
+  };
+
+  for (uint32_t k = 1; k < B.dpCount; k++) {
+    const DpSeg G = dpSegs[B.dpFirst + k];
+    const int32_t lo = (int32_t)G.lo, hi = (int32_t)G.hi;
+    const uint4 st = segState[B.dpFirst + k - 1];  // exact state below the segment above
+    uint32_t lits = st.x, litBump = st.y;
+    uint32_t costNext = exact_above((uint32_t)hi + 1);
+    uint32_t cbuf = exact_above((uint32_t)hi + 1 + ((lane - (uint32_t)hi - 1u) & 63u));
+    // exact cost of j > i: this pass's own results (ring / HBM) inside the segment, above it the table
+    auto cost_at = [&](int32_t i, int32_t j) -> uint32_t {
+      if (j > hi) return exact_above((uint32_t)j);
+      return j - i < kRing ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
+    };
+    uint32_t prevDelta = 0;
+    int32_t runTop = hi;
+    int32_t conv = lo;
+    uint32_t convDelta = 0;
+    bool done = false;
+    for (int32_t h = hi; h >= lo && !done; h -= 64) {
+      const int32_t ip = h - (int32_t)lane;
+      const bool in = ip >= lo;
+      const uint32_t cL = in ? L[ip] : 0u, cD = in ? (uint32_t)D[ip] : 0u;
+      const uint32_t cS = in ? S[ip] : 0u, cC = in ? cost[ip] : 0u, cR = in ? R[ip] : 0u;
+      for (uint32_t t = 0; t < 64; t++) {
+        const int32_t i = h - (int32_t)t;
+        if (i < lo) break;
+        const uint32_t Lk = rdlane(cL, t), Dk = rdlane(cD, t);
+        lits++;
+        uint32_t minCost = costNext + 1;
+        if (lits == litBump) {
+          minCost++;
+          litBump += 255;
+        }
+        uint32_t best = 1;
+        if (Lk >= (uint32_t)kMinMatch) {
+          if (Lk >= kSameLetter && Dk == 1) {
+            best = Lk;
+            minCost = cost_at(i, i + (int32_t)Lk) + 4 + (Lk - 19) / 255;
+          } else {
+            const uint32_t len = ((lane - (uint32_t)i - 1u) & 63u) + 1u;
+            const uint32_t top = Lk < 64 ? Lk : 64u;
+            const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
+            const uint32_t kmin = wave_min_fast(len - 4u <= top - 4u ? key : 0xFFFFFFFFu);
+            if ((kmin >> 6) <= minCost) {
+              minCost = kmin >> 6;
+              best = 64u - (kmin & 63u);
+            }
+            for (uint32_t b = 65; b <= Lk; b += 64) {
+              const uint32_t ln = b + lane;
+              uint32_t k2 = 0xFFFFFFFFu;
+              if (ln <= Lk) k2 = ((cost_at(i, i + (int32_t)ln) + len_extra(ln)) << 6) | (63u - lane);
+              const uint32_t km = wave_min_fast(k2);
+              if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
+                minCost = km >> 6;
+                best = b + (63u - (km & 63u));
+              }
+            }
+          }
+        }
+        const uint32_t specBest = rdlane(cS, t), specCost = rdlane(cC, t), rch = rdlane(cR, t);
+        if (lane == 0) {
+          S[i] = best;
+          cost[i] = minCost;
+          ring[i & (kRing - 1)] = minCost;
+        }
+        cbuf = lane == ((uint32_t)i & 63u) ? minCost : cbuf;
+        costNext = minCost;
+        const uint32_t delta = minCost - specCost;
+        if (i == hi || delta != prevDelta) runTop = i;
+        prevDelta = delta;
+        if (best != 1) {
+          lits = 0;
+          litBump = 15;
+          const int32_t need = (int32_t)rch > i ? (int32_t)rch : i;
+          if (specBest != 1 && runTop >= need) {
+            conv = i;
+            convDelta = delta;
+            done = true;
+            break;
+          }
+        }
+      }
+    }
+    if (lane == 0) {
+      convTab[k] = (uint32_t)conv;
+      deltaTab[k] = convDelta;
+      // not converged: the state below the segment is this pass's own
+      if (!done) segState[B.dpFirst + k] = make_uint4(lits, litBump, 0u, 0u);
+    }
+    __syncthreads();
+  }
 }
 
 // ================================================================================================
@@ -1354,13 +1494,18 @@ void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
   }
 }
 
-void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const Interval* iv, const uint32_t* ivCount,
-                  uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase, uint32_t* cost, int* status,
-                  hipStream_t s)
+void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
+                  const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
+                  uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, int* status, hipStream_t s)
 {
-  if (nblocks)
-    hipLaunchKernelGGL(k_parse, dim3(nblocks), dim3(64), 0, s, in, blocks, iv, ivCount, maxChain, mlen, mdist, matchBase, cost,
-                       status);
+  (void)in;
+  if (!nblocks) return;
+  hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, maxChain, mlen, matchBase, sel, status);
+  if (maxChain <= (uint32_t)kGreedyMax || !ndp) return;
+  hipLaunchKernelGGL(k_dp_spec, dim3(ndp), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
+                     segState);
+  hipLaunchKernelGGL(k_dp_fix, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
+                     segState);
 }
 
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
