@@ -74,6 +74,14 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
 }
 
 // DPP row (16-lane) permutations
+// v_writelane (no clang builtin on this toolchain; the LLVM intrinsic by name): lane `l` of v
+// becomes the uniform `x`
+extern "C" __device__ int sz4_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t wrlane(uint32_t v, uint32_t x, uint32_t l)
+{
+  return (uint32_t)sz4_llvm_writelane((int)x, (int)l, (int)v);
+}
+
 template <int kCtrl>
 __device__ __forceinline__ uint32_t dpp(uint32_t v)
 {
@@ -965,16 +973,23 @@ __global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, c
   }
 }
 
-__global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
-                                                const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
-                                                uint64_t matchBase, uint32_t* __restrict__ costAll,
-                                                uint32_t* __restrict__ sel, uint32_t* __restrict__ reach,
-                                                uint4* __restrict__ segState)
+constexpr int kSpecWaves = 4;  // independent segments per workgroup (workgroup slots, not LDS, bound occupancy)
+
+__global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __restrict__ blocks,
+                                                             const DpSeg* __restrict__ dpSegs, uint32_t ndp,
+                                                             const uint32_t* __restrict__ mlen,
+                                                             const uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                                             uint32_t* __restrict__ costAll, uint32_t* __restrict__ sel,
+                                                             uint32_t* __restrict__ reach, uint4* __restrict__ segState)
 {
-  __shared__ uint32_t ring[kRing];
-  const DpSeg G = dpSegs[blockIdx.x];
+  __shared__ uint32_t rings[kSpecWaves][kRing];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform
+  const uint32_t segIdx = blockIdx.x * kSpecWaves + wave;
+  if (segIdx >= ndp) return;  // whole wavefronts only; the waves never synchronize
+  uint32_t* ring = rings[wave];
+  const DpSeg G = dpSegs[segIdx];
   const Block B = blocks[G.block];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
   const uint64_t base = B.start - matchBase;
   const uint32_t* L = mlen + base;
   const uint16_t* D = mdist + base;
@@ -998,15 +1013,23 @@ __global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks
     }
   }
 
-  // decision state, uniform but kept in vector registers (no SGPR round trips on the chain);
-  // the top segment starts exactly (costs past the block end are 0, five trailing literals)
-  uint32_t litsV = G.k == 0 ? (uint32_t)kTailLiterals : 0u;
-  uint32_t bumpV = 15;    // literal-run length at which a literal costs one more byte (15, 270, ...)
-  uint32_t costV = 0;     // cost[i + 1]
-  uint32_t cbuf = 0;      // cost[j] of the 64 positions above i, in lane j & 63
+  // win: lane l holds cost[i0 + 1 + l] << 6 for the batch start i0.  For position i0 - r lane l
+  // is match length l + 1 + r, so a candidate key is win + kLen[r] (a per-lane constant).
+  // Above the segment the costs are the guess 0 (exact for k = 0).
+  uint32_t kLen[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const uint32_t len = lane + 1u + (uint32_t)r;
+    // key = (cost + 3 [+1 from length 19]) << 6 | (64 - len): minimum = cheapest, then longest
+    kLen[r] = len < (uint32_t)kMinMatch ? 0x80000000u : (((3u + (len >= 19u ? 1u : 0u)) << 6) + (64u - len));
+  }
+  uint32_t win = 0;
+  // decision state (uniform, scalar)
+  uint32_t lits = G.k == 0 ? (uint32_t)kTailLiterals : 0u;
+  uint32_t litBump = 15;  // literal-run length at which a literal costs one more byte (15, 270, ...)
+  uint32_t costNext = 0;  // cost[i + 1]
   uint32_t nextL = segHi - (int32_t)lane >= segLo ? L[segHi - lane] : 0u;
-  uint32_t nextD = segHi - (int32_t)lane >= segLo ? (uint32_t)D[segHi - lane] : 0u;
-  // cost read-back above the register window: above the segment the guess is 0 (exact for k = 0)
+  // cost read-back above the register window
   auto far_cost = [&](int32_t i, uint32_t ln) -> uint32_t {
     const int32_t j = i + (int32_t)ln;
     if (j > segHi) return 0u;
@@ -1015,63 +1038,63 @@ __global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks
 
   for (int32_t hi = segHi; hi >= segLo; hi -= 64) {
     const int32_t lo = hi - 63 > segLo ? hi - 63 : segLo;
-    // opaque copies: the loop below must not wait for the prefetch issued right after
-    uint32_t myL, myD;
+    // opaque copy: the loop below must not wait for the prefetch issued right after
+    uint32_t myL;
     asm volatile("v_mov_b32 %0, %1" : "=v"(myL) : "v"(nextL));
-    asm volatile("v_mov_b32 %0, %1" : "=v"(myD) : "v"(nextD));
     const int32_t iN = hi - 64 - (int32_t)lane;
     nextL = iN >= segLo ? L[iN] : 0u;  // prefetch the next chunk
-    nextD = iN >= segLo ? (uint32_t)D[iN] : 0u;
-    uint32_t myBest = 1;
-    // Four positions per trip: the candidates of q (lengths >= 4) only read cost[q+4 ..], so
-    // at the start of the trip i0 the minima of i0, i0-1, i0-2, i0-3 are all computable.  Their
-    // four wavefront reductions are independent and interleave; the decisions follow.
+    // per position hi - t in lane t: its best key (0 = slow path, see bestBuf), its cost, its choice
+    uint32_t kvBuf = 0xFFFFFFFFu, mcBuf = 0, bestBuf = 1;
     for (uint32_t t = 0; t < 64; t += 4) {
       const int32_t i0 = hi - (int32_t)t;
       if (i0 < lo) break;
-      uint32_t Lr[4], Dr[4], kv[4];
-      bool slow = i0 - 3 < lo;  // partial batch at the segment start
-      // cbuf lane -> match length for q = i0 - r: ((lane - q - 1) & 63) + 1 in 1..64
-      const uint32_t dl = lane - (uint32_t)i0 - 1u;
+      // next batch's window, shifted by four lanes (lanes 0-3 are refilled below)
+      uint32_t nwin = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 4u) << 2), (int)win);
+      uint32_t Lr[4], kv[4], mcost[4];
+      uint32_t maxL = 0;
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         Lr[r] = i0 - r >= lo ? rdlane(myL, t + r) : 0u;
-        Dr[r] = i0 - r >= lo ? rdlane(myD, t + r) : 0u;
-        slow |= Lr[r] > 64u;  // lengths beyond the register window (includes same-letter runs)
-        const uint32_t len = ((dl + (uint32_t)r) & 63u) + 1u;
-        const uint32_t top = Lr[r] < 64 ? Lr[r] : 64u;
-        // key = (cost + 3 [+1 from length 19]) << 6 | (64 - len): minimum = cheapest, then longest
-        const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
-        kv[r] = (len - 4u <= top - 4u && top >= 4u) ? key : 0xFFFFFFFFu;
+        maxL = Lr[r] > maxL ? Lr[r] : maxL;
       }
 #pragma unroll
-      for (int r = 0; r < 4; r++) kv[r] = wave_min_all(kv[r]);
-      if (!slow) {
-        // the decision chain, entirely in (uniform) vector registers and branch-free
+      for (int r = 0; r < 4; r++) {
+        // valid candidates: lengths 4 .. min(Lr[r], 64) (length l + 1 + r); longer ones are the slow path's
+        const uint32_t top = Lr[r] < 64u ? Lr[r] : 64u;
+        kv[r] = lane + 1u + (uint32_t)r <= top ? win + kLen[r] : 0xFFFFFFFFu;
+      }
+      if (maxL <= 16u) {
+        // every candidate sits in row 0
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const uint32_t i = (uint32_t)(i0 - r);
-          litsV++;
-          const bool bump = litsV == bumpV;
-          bumpV = bump ? bumpV + 255u : bumpV;
-          const uint32_t lit = costV + 1u + (bump ? 1u : 0u);
-          const uint32_t mc = kv[r] >> 6;
-          const bool use = kv[r] != 0xFFFFFFFFu && mc <= lit;  // ties go to the match, and the longer one
-          const uint32_t minCost = use ? mc : lit;
-          const uint32_t best = use ? 64u - (kv[r] & 63u) : 1u;
-          litsV = use ? 0u : litsV;
-          bumpV = use ? 15u : bumpV;
-          costV = minCost;
-          cbuf = lane == (i & 63u) ? minCost : cbuf;
-          myBest = lane == t + (uint32_t)r ? best : myBest;
-        }
+        for (int r = 0; r < 4; r++) kv[r] = rdlane(row_min(kv[r]), 0);
       } else {
-        uint32_t lits = rdlane(litsV, 0), litBump = rdlane(bumpV, 0), costNext = rdlane(costV, 0);
+#pragma unroll
+        for (int r = 0; r < 4; r++) kv[r] = wave_min_fast(kv[r]);
+      }
+      // fast batch: four whole positions, no literal-length bump reachable, no length beyond 64
+      if (i0 - 3 >= lo && maxL <= 64u && lits + 4u < litBump) {
+        bool anyMatch = false;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
+          // a match wins ties; invalid keys decode to costs no literal path reaches
+          const uint32_t mc = kv[r] >> 6;
+          const uint32_t c = min(costNext + 1u, mc);
+          const bool use = c == mc;
+          lits = use ? 0u : lits + 1u;
+          anyMatch |= use;
+          costNext = c;
+          mcost[r] = c;
+          kvBuf = wrlane(kvBuf, kv[r], t + (uint32_t)r);
+          mcBuf = wrlane(mcBuf, c, t + (uint32_t)r);
+        }
+        litBump = anyMatch ? 15u : litBump;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          mcost[r] = 0;
           const int32_t i = i0 - r;
           if (i < lo) break;
-          const uint32_t Lk = Lr[r], Dk = Dr[r];
+          const uint32_t Lk = Lr[r];
           lits++;
           uint32_t minCost = costNext + 1;
           if (lits == litBump) {
@@ -1080,12 +1103,12 @@ __global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks
           }
           uint32_t best = 1;
           if (Lk >= (uint32_t)kMinMatch) {
-            if (Lk >= kSameLetter && Dk == 1) {
+            if (Lk >= kSameLetter && D[i] == 1) {
               best = Lk;
               const int32_t j = i + (int32_t)Lk;  // far back: spilled
               minCost = (j > segHi ? 0u : ld_fresh(&cost[j])) + 4 + (Lk - 19) / 255;
             } else {
-              const uint32_t kmin = rdlane(kv[r], 0);
+              const uint32_t kmin = kv[r];
               if ((kmin >> 6) <= minCost) {
                 minCost = kmin >> 6;
                 best = 64u - (kmin & 63u);
@@ -1103,29 +1126,32 @@ __global__ __launch_bounds__(64) void k_dp_spec(const Block* __restrict__ blocks
               }
             }
           }
-          cbuf = lane == ((uint32_t)i & 63u) ? minCost : cbuf;
-          myBest = lane == t + (uint32_t)r ? best : myBest;
+          mcost[r] = minCost;
           costNext = minCost;
           if (best != 1) {
             lits = 0;
             litBump = 15;
           }
+          kvBuf = wrlane(kvBuf, 0u, t + (uint32_t)r);
+          mcBuf = wrlane(mcBuf, minCost, t + (uint32_t)r);
+          bestBuf = wrlane(bestBuf, best, t + (uint32_t)r);
         }
-        litsV = lits;
-        bumpV = litBump;
-        costV = costNext;
       }
+      // lanes 0-3 of the next window are positions i0-3 .. i0
+#pragma unroll
+      for (int r = 0; r < 4; r++) nwin = wrlane(nwin, mcost[r] << 6, 3u - (uint32_t)r);
+      win = nwin;
     }
-    // flush: this chunk's choices, and its costs to the ring and the HBM spill
+    // flush: choices (a position took its best key iff its cost is that key's), costs to ring and HBM
     const int32_t iMine = hi - (int32_t)lane;
-    if (iMine >= lo) S[iMine] = myBest;
-    const int32_t jl = lo + (int32_t)((lane - (uint32_t)lo) & 63u);  // position held by this lane
-    if (jl <= hi) {
-      ring[jl & (kRing - 1)] = cbuf;
-      cost[jl] = cbuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
+    if (iMine >= lo) {
+      const uint32_t best = kvBuf == 0u ? bestBuf : ((kvBuf >> 6) == mcBuf ? 64u - (kvBuf & 63u) : 1u);
+      S[iMine] = best;
+      ring[iMine & (kRing - 1)] = mcBuf;
+      cost[iMine] = mcBuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
     }
   }
-  if (lane == 0) segState[blockIdx.x] = make_uint4(rdlane(litsV, 0), rdlane(bumpV, 0), 0u, 0u);
+  if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, 0u, 0u);
 }
 
 __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
@@ -1502,8 +1528,8 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
   if (!nblocks) return;
   hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, maxChain, mlen, matchBase, sel, status);
   if (maxChain <= (uint32_t)kGreedyMax || !ndp) return;
-  hipLaunchKernelGGL(k_dp_spec, dim3(ndp), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
-                     segState);
+  hipLaunchKernelGGL(k_dp_spec, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs, ndp,
+                     mlen, mdist, matchBase, cost, sel, reach, segState);
   hipLaunchKernelGGL(k_dp_fix, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
                      segState);
 }
