@@ -226,7 +226,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
     // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
     if (maxChain > 0 && (e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)))
       return c->fail(SZ4_E_DEVICE, "clear matches", e);
-    launch_find(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+    launch_find(in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                 c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
   }
   mark(c, 3, s);

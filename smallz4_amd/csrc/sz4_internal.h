@@ -77,7 +77,7 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
                  const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
                  uint32_t* rank, hipStream_t s);
 void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
-                 const Interval* iv, const uint32_t* ivCount, const uint2* elem, const uint2* compact,
+                 const Interval* iv, const uint32_t* ivCount, const uint2* compact,
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  bool ldsWindow, hipStream_t s);
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,

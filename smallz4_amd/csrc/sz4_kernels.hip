@@ -18,7 +18,7 @@
 #include "sz4_internal.h"
 
 #ifndef SZ4_DIAG
-#define SZ4_DIAG 0  // diagnostic timing builds only (wrong output): 1 = no parse reductions, 2 = no parse chain
+#define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
 #endif
 
 namespace sz4 {
@@ -74,6 +74,14 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
 }
 
 // DPP row (16-lane) permutations
+#if SZ4_DIAG == 3
+__device__ uint64_t sz4_diag[1 << 20];
+extern "C" int sz4_diag_read(uint64_t* out, uint64_t n)
+{
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sz4_diag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // v_writelane (no clang builtin on this toolchain; the LLVM intrinsic by name): lane `l` of v
 // becomes the uniform `x`
 extern "C" __device__ int sz4_llvm_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
@@ -513,15 +521,26 @@ __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t 
 }
 
 // ================================================================================================
-// k_find_sorted (pass 1): one lane per target, targets taken in SORTED order.  A lane's
-// candidates are the same-key slots just below its own inside its hash group, so the 64 lanes of a
-// wavefront read neighbouring slots (coalesced) and lanes of one big group loop the same number
-// of times.  Each lane runs the reference's own nearest-first scan (smallz4.h:190-252): phase-1
-// check at the length it must reach, extension, strict improvement, step limit.  The extension is
-// capped at kLongCap bytes: a target whose best reaches the cap keeps the marker kLongMatch and is
-// finished by k_find (pass 2), which walks long repeats in text order with the carried match.
+// k_find_sorted (pass 1): a wavefront takes 64 consecutive SORTED slots (lane = target).  A
+// target's candidates are the slots below it in its hash group, nearest first, and each is checked
+// on its first 12 bytes, which every lane keeps in registers for its own slot:
+//   1. candidates inside the chunk come through a shift register (DPP wave_shr:1): after s shifts
+//      lane l holds slot first + l - s, so every lane sees its own candidates in order;
+//   2. candidates below the chunk can only belong to the group that started before it, so they
+//      are the same for all of its lanes: 64 at a time into registers, one v_readlane each.
+// -9 takes the maximum of (prefix << 17 | slot): the reference's nearest-first strict-improvement
+// walk (smallz4.h:190-252) ends on the nearest candidate of maximal prefix, so no order is needed;
+// candidates whose 12 bytes all match are queued per wavefront and extended from the text 64 at a
+// time.  Bounded chains keep the ordered walk (masked "first bestLen+1 bytes" test, strict
+// improvement, step limit).  Prefixes are capped at kLongCap: a target reaching it keeps the marker
+// kLongMatch and is finished by k_find (pass 2), which walks long repeats in text order.
 // ================================================================================================
 constexpr uint32_t kLongCap = 32;
+constexpr uint32_t kSatQ = 128;  // saturated-candidate queue per wavefront (flushed at 64)
+// broadcast chunk list: >= slots / 64 + number of groups of >= 64 slots (64 Ki slots with the LDS
+// window, 128 Ki otherwise)
+template <bool kLds>
+constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 
 // per-slot arrays written by k_sort: u16 when the segment's window fits 16 bits (same predicate there)
@@ -536,7 +555,7 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 }
 
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                               const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                               const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                               uint32_t maxChain, uint32_t* __restrict__ mlen,
@@ -544,9 +563,16 @@ __global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __r
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
+  // -9: per wavefront, candidates whose first 12 bytes match (lane << 17 | slot) and the best
+  // exact key of each lane among them
+  __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
+  __shared__ uint32_t s_satBest[kFindThreads / 64][64];
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t waveId = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  uint32_t* satQ = s_satQ[waveId];
+  uint32_t* satBest = s_satBest[waveId];
   const void* compact = compactAll + S.elemOff;
   // number of sorted slots: window positions minus shortcut-interval positions
   const uint32_t W = (uint32_t)(S.s1 - S.w0);
@@ -565,6 +591,10 @@ __global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __r
   const uint32_t E = W - excluded;
   const bool small = compact_small(S);
 
+#if SZ4_DIAG == 3
+  const uint64_t t0 = __builtin_readcyclecounter();
+  uint64_t dB = 0, dL = 0, dBi = 0, dLi = 0;
+#endif
   if (tid == 0) s_next = 0;
   Bytes<kLds> src;
   if constexpr (kLds) {
@@ -586,83 +616,275 @@ __global__ __launch_bounds__(kFindThreads) void k_find_sorted(const uint8_t* __r
   }
   const uint64_t stopAbs = B.end - kTailLiterals;
   const bool unlimited = maxChain >= 65535u;
+  // every distance inside a segment of at most 64 KiB is in the window, unless the lookback cut applies
+  const bool needWin = (S.s1 - S.w0 > 65536u) || cut != kNone;
+  const uint32_t nChunks = (E + 63) / 64;
 
   while (true) {
-    uint32_t chunkIdx = 0;
-    if (lane == 0) chunkIdx = atomicAdd(&s_next, 1u);
-    chunkIdx = rdlane(chunkIdx, 0);
-    const uint32_t first = chunkIdx * 64;
-    if (first >= E) break;
+    uint32_t item = 0;
+    if (lane == 0) item = atomicAdd(&s_next, 1u);
+    item = rdlane(item, 0);
+    if (item >= nChunks) break;
+    const uint32_t first = item * 64;
+    const uint32_t count = E - first < 64 ? E - first : 64;
     const uint32_t slot = first + lane;
-    uint64_t p = 0;
-    uint32_t gs = 0;
-    bool active = slot < E;
+    // every lane's slot is a candidate for the lanes above it: its data is loaded even when the
+    // slot itself is not a target (window-only positions)
+    const bool inChunk = lane < count;
+    const uint32_t myRel = inChunk ? slot_pos(compact, small, slot) : 0u;
+    const uint32_t gs = inChunk ? slot_gs(compact, small, E, slot) : slot;
+    const uint64_t p = S.w0 + myRel;
+    const uint32_t me0 = inChunk ? src.ld4(p) : 0u, me1 = inChunk ? src.ld4(p + 4) : 0u;
+    const uint32_t me2 = inChunk ? src.ld4(p + 8) : 0u;
+    const bool active = inChunk && p >= S.s0;  // window-only positions are candidates, not targets
+    uint32_t room = 0, lbRel = 0, limit = 0;
     if (active) {
-      p = S.w0 + slot_pos(compact, small, slot);
-      gs = slot_gs(compact, small, E, slot);
-      active = p >= S.s0;  // else a window-only position (previous segment / previous block)
-    }
-    if (active) {
-      const uint32_t key = src.ld4(p);
-      const uint32_t room = (uint32_t)(stopAbs - p);
+      room = (uint32_t)(stopAbs - p);
       uint64_t lb = p > kWindow ? p - kWindow : 0;
-      if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
-      const uint32_t limit = room < kLongCap ? room : kLongCap;
-      uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
-      bool isLong = false, run = true;
-      int64_t j = (int64_t)slot - 1;
-      while (run && j >= (int64_t)gs) {
-        // four candidates per trip: their loads are independent
-        uint32_t cp[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          cp[u] = j - u >= (int64_t)gs ? slot_pos(compact, small, (uint32_t)(j - u)) : 0xFFFFFFFFu;
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          if (run) {
-            const uint64_t c = S.w0 + cp[u];
-            const uint32_t need = bestLen + 1 < 4 ? 4 : bestLen + 1;
-            if (cp[u] == 0xFFFFFFFFu || c < lb || need > room) {
-              run = false;
-            } else if (src.ld4(c) != key) {
-              // same hash, different four bytes: not on the reference's chain
-            } else {
-              // phase 1: the four bytes ending at `need` decide most candidates, then the rest
-              bool same = need <= 4 || src.ld4(p + need - 4) == src.ld4(c + need - 4);
-              for (uint32_t k = 4; same && k + 4 < need; k += 4) same = src.ld4(p + k) == src.ld4(c + k);
-              if (same) {
-                // phase 2: extend up to the cap
-                uint32_t k = need;
-                bool open = true;
-                while (open && k < limit) {
-                  const uint32_t x = src.ld4(p + k) ^ src.ld4(c + k);
-                  if (x) {
-                    k += (uint32_t)__builtin_ctz(x) >> 3;
-                    open = false;
-                  } else {
-                    k += 4;
-                  }
-                }
-                if (k > limit) k = limit;
-                bestLen = k;
-                bestDist = (uint32_t)(p - c);
-                if (k >= limit && limit < room) {
-                  isLong = true;
-                  run = false;
-                } else if (--steps == 0 || bestLen >= room) {
-                  run = false;
-                }
-              }
-            }
+      if (cut != kNone && ref_hash(me0) == cutHash && cut > lb) lb = cut;
+      lbRel = lb > S.w0 ? (uint32_t)(lb - S.w0) : 0u;
+      limit = room < kLongCap ? room : kLongCap;
+    }
+    uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
+    bool isLong = false, run = active && bestLen < room && gs < slot;
+    // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
+    uint32_t m1 = 0, m2 = 0;
+    // the candidate at cpos passed the mask test: its exact prefix (extended past 12 from the text)
+    auto improve = [&](uint64_t cpos, uint32_t k1, uint32_t k2) {
+#if SZ4_DIAG == 3
+      dBi++;
+#endif
+      const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
+      uint32_t kk = x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3) : 12u;
+      if (kk == 12u) {
+        bool open = true;
+        while (open && kk < limit) {
+#if SZ4_DIAG == 3
+          dLi++;
+#endif
+          const uint32_t x = src.ld4(p + kk) ^ src.ld4(cpos + kk);
+          if (x) {
+            kk += (uint32_t)__builtin_ctz(x) >> 3;
+            open = false;
+          } else {
+            kk += 4;
           }
         }
-        j -= 4;
       }
+      if (kk > limit) kk = limit;
+      if (kk > bestLen) {
+        bestLen = kk;
+        bestDist = (uint32_t)(p - cpos);
+        if (kk >= limit && limit < room) {
+          isLong = true;
+          run = false;
+        } else if (--steps == 0 || bestLen >= room) {
+          run = false;
+        }
+        const uint32_t nb = bestLen + 1;
+        m1 = nb <= 4 ? 0u : nb >= 8 ? 0xFFFFFFFFu : (1u << (8 * (nb - 4))) - 1u;
+        m2 = nb <= 8 ? 0u : nb >= 12 ? 0xFFFFFFFFu : (1u << (8 * (nb - 8))) - 1u;
+      }
+    };
+    auto test = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
+      return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
+    };
+    if (unlimited) {
+      // -9: the reference's nearest-first strict-improvement walk over every candidate ends on
+      // the nearest candidate of maximal common prefix, so the result is the maximum of
+      // key = prefix << 17 | slot (slots grow with position inside a group), order-free and
+      // branch-free.  Prefixes are exact up to 12 bytes; candidates reaching 12 are queued and
+      // extended from the text in batches of 64 (one per lane).
+      uint32_t bestKey = 0;
+      uint32_t qn = 0;
+      satBest[lane] = 0;
+      const uint32_t cap12 = limit < 12u ? limit : 12u;
+      auto flush = [&]() {
+        // lane t extends queue entry base + t: target = lane (e >> 17), candidate slot e & 0x1FFFF
+        for (uint32_t base = 0; base < qn; base += 64) {
+        const uint32_t e = base + lane < qn ? satQ[base + lane] : 0u;
+        const uint32_t tl = e >> 17, cs = e & 0x1FFFFu;
+        const uint32_t tRel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)myRel);
+        const uint32_t tLim = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)limit);
+        if (base + lane < qn) {
+          const uint64_t tp = S.w0 + tRel, cp = S.w0 + slot_pos(compact, small, cs);
+          uint32_t kk = 12;
+          bool open = true;
+          while (open && kk < tLim) {
+            const uint32_t x = src.ld4(tp + kk) ^ src.ld4(cp + kk);
+            if (x) {
+              kk += (uint32_t)__builtin_ctz(x) >> 3;
+              open = false;
+            } else {
+              kk += 4;
+            }
+          }
+          if (kk > tLim) kk = tLim;
+          atomicMax(&satBest[tl], (kk << 17) | cs);
+        }
+        }
+        qn = 0;
+      };
+      // one candidate for this lane: slot cs with first 12 bytes k0..k2
+      auto visit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
+        const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
+        const uint32_t f1 = min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
+        const uint32_t f2 = min((uint32_t)(__ffs(x2) - 1) >> 3, 4u);
+        uint32_t lcp = 4u + f1 + (f1 == 4u ? f2 : 0u);
+        lcp = lcp < cap12 ? lcp : cap12;
+        const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+        const uint64_t sat = __ballot(mine && x0 == 0u && lcp == 12u && limit > 12u);
+        if (sat) {
+          const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
+          if ((sat >> lane) & 1ull) satQ[at] = (lane << 17) | cs;
+          qn += (uint32_t)__builtin_popcountll(sat);
+          if (qn >= 64) flush();
+        }
+      };
+      // 1. inside the chunk: shift register (after s shifts lane l holds slot first + l - s)
+      {
+        const int32_t lo1 = (int32_t)(gs > first ? gs : first);
+        uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
+        int32_t cl = (int32_t)slot;
+        bool walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
+        while (__ballot(walk)) {
+#if SZ4_DIAG == 3
+          dL++;
+#endif
+          rRel = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rRel, kWaveShr1, 0xF, 0xF, false);
+          r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
+          r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
+          r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
+          cl--;
+          if (needWin && walk && rRel < lbRel) walk = run = false;
+          visit(walk, (uint32_t)cl, r0, r1, r2);
+          walk = walk && cl > lo1;
+        }
+        run = run && (int32_t)gs < (int32_t)first;
+      }
+      // 2. below the chunk: the group that started before it, one uniform candidate per step
+      if (__ballot(run)) {
+        const int32_t gsB = (int32_t)rdlane(gs, 0);
+        int32_t cBase = (int32_t)first - 1;
+        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? slot_pos(compact, small, (uint32_t)(cBase - (int32_t)lane)) : 0u;
+        while (cBase >= gsB && __ballot(run)) {
+          uint32_t fRel;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(fRel) : "v"(nextBlk));
+          const int32_t cn = cBase - 64 - (int32_t)lane;
+          nextBlk = cn >= gsB ? slot_pos(compact, small, (uint32_t)cn) : 0u;
+          const uint64_t fp = S.w0 + fRel;
+          const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
+          const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
+          for (int32_t k = 0; k < n; k++) {
+#if SZ4_DIAG == 3
+            dB++;
+#endif
+            if (needWin && run && rdlane(fRel, k) < lbRel) run = false;
+            visit(run, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+          }
+          cBase -= 64;
+        }
+      }
+      if (qn) flush();
+      const uint32_t sb = satBest[lane];
+      bestKey = sb > bestKey ? sb : bestKey;
+      const uint32_t bl = bestKey >> 17;
+      if (bl >= 4u) {
+        bestLen = bl;
+        bestDist = (uint32_t)(p - (S.w0 + slot_pos(compact, small, bestKey & 0x1FFFFu)));
+        isLong = bl >= limit && limit < room;
+      }
+    } else {
+    // 1. candidates inside the chunk, nearest first: a shift register -- after s shifts lane l holds
+      //    slot first + l - s -- walked while some lane's candidate is >= max(its group start, first)
+      {
+        const int32_t lo1 = (int32_t)(gs > first ? gs : first);
+        uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
+        int32_t cl = (int32_t)slot;
+        bool walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
+        while (__ballot(walk)) {
+#if SZ4_DIAG == 3
+          dL++;
+#endif
+          rRel = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rRel, kWaveShr1, 0xF, 0xF, false);
+          r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
+          r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
+          r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
+          cl--;
+          if (walk) {
+            if (needWin && rRel < lbRel) run = false;
+            if (run && test(r0, r1, r2) == 0u) improve(S.w0 + rRel, r1, r2);
+          }
+          walk = walk && run && cl > lo1;
+        }
+        // a lane whose group starts inside the chunk has seen all its candidates
+        run = run && (int32_t)gs < (int32_t)first;
+      }
+      // 2. below the chunk: only the group that started before it (lanes 0..) is left, and every
+      //    one of its lanes takes the same candidate -- 64 at a time (lane k: slot cBase - k, its
+      //    position prefetched one block ahead, its first 12 bytes from the window), four per test
+      if (__ballot(run)) {
+        const int32_t gsB = (int32_t)rdlane(gs, 0);
+        int32_t cBase = (int32_t)first - 1;
+        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? slot_pos(compact, small, (uint32_t)(cBase - (int32_t)lane)) : 0u;
+        while (cBase >= gsB && __ballot(run)) {
+          uint32_t fRel;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(fRel) : "v"(nextBlk));
+          const int32_t cn = cBase - 64 - (int32_t)lane;
+          nextBlk = cn >= gsB ? slot_pos(compact, small, (uint32_t)cn) : 0u;
+          const uint64_t fp = S.w0 + fRel;
+          const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
+          const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
+          int32_t k = 0;
+          if (!needWin) {
+            for (; k + 4 <= n; k += 4) {
+#if SZ4_DIAG == 3
+              dB += 4;
+#endif
+              uint32_t a0[4], a1[4], a2[4], t[4];
+#pragma unroll
+              for (int u = 0; u < 4; u++) {
+                a0[u] = rdlane(f0, k + u);
+                a1[u] = rdlane(f1, k + u);
+                a2[u] = rdlane(f2, k + u);
+                t[u] = test(a0[u], a1[u], a2[u]);
+              }
+              if (__ballot(run && min(min(t[0], t[1]), min(t[2], t[3])) == 0u)) {
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                  if (run && test(a0[u], a1[u], a2[u]) == 0u) improve(S.w0 + rdlane(fRel, k + u), a1[u], a2[u]);
+              }
+              if (!__ballot(run)) break;
+            }
+          }
+          for (; k < n && __ballot(run); k++) {
+#if SZ4_DIAG == 3
+            dB++;
+#endif
+            const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k), crel = rdlane(fRel, k);
+            if (needWin && run && crel < lbRel) run = false;
+            if (run && test(k0, k1, k2) == 0u) improve(S.w0 + crel, k1, k2);
+          }
+          cBase -= 64;
+        }
+      }
+    }
+    if (active) {
       const uint64_t idx = p - matchBase;
       mlen[idx] = isLong ? kLongMatch : (bestDist ? bestLen : 0u);
       mdist[idx] = (uint16_t)bestDist;
     }
   }
+#if SZ4_DIAG == 3
+  const uint64_t t2 = __builtin_readcyclecounter();
+  const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
+  if (lane == 0 && w * 8 + 8 <= (1u << 20)) {
+    uint64_t* d = sz4_diag + w * 8;
+    d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = 0; d[7] = 0;
+  }
+#endif
 }
 
 template <bool kLds>
@@ -1497,7 +1719,7 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
 uint32_t find_lds_bytes() { return 65536 + 16; }
 
 void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
-                 const uint32_t* ivCount, const uint2* elem, const uint2* compact, const uint32_t* rank, uint32_t maxChain,
+                 const uint32_t* ivCount, const uint2* compact, const uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
 {
   if (!nsegs) return;
