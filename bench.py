@@ -14,7 +14,7 @@ Also reported:
   byte_diff     differing bytes between the GPU frame and the reference's output for
                 every block (oracle/_ref, compiled from the reference sources; the C
                 restatement when _ref is absent), all blocks, every rank
-  roofline      dominant kernel (k_find), HIP-event timed on its stream
+  roofline      dominant kernel (k_find_sorted), HIP-event timed on its stream
   cpu_baseline  the reference itself on this host, one thread, bounded sample
 """
 from __future__ import annotations
@@ -162,11 +162,12 @@ def main():
 
     if rank == 0:
         value = world * nbytes * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel k_find: its compulsory I/O per searched
-        # position = input byte (1) + sorted (key, pos) element (8) + rank (4) + match written (6)
-        find_ms = stages.get("find", 0.0)
+        # roofline of the dominant kernel k_find_sorted: its compulsory HBM bytes
+        # per searched position = text byte (1) + sorted slot arrays, u16 position and group start (4)
+        # + match written, u32 length and u16 distance (6) = 11
+        find_ms = stages.get("find_sorted", 0.0)
         targets = sum(max(0, min(args.block_size, nbytes - o) - 11) for o in range(0, nbytes, args.block_size))
-        alg_bytes = nbytes + 18 * targets
+        alg_bytes = nbytes + 4 * nbytes + 6 * targets
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "r01_find_hbm_bytes.json")
@@ -195,7 +196,7 @@ def main():
             "verified_against": kind,
             "compression_ratio": round(size / nbytes, 5),
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
-            "roofline": {"kernel": "k_find", "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": "k_find_sorted", "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes},
         }

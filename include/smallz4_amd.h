@@ -84,7 +84,8 @@ uint64_t sz4_lz4_bound(uint64_t n, int legacy);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured
  * with HIP events on the call's stream.  stage_ms[0..n) receives
- * {runs, sort, find, parse, assemble}; returns the number of stages. */
+ * {runs, sort, find_sorted, find_long, parse, assemble} (find_sorted is the
+ * k_find_sorted kernel alone); returns the number of stages. */
 int sz4_last_stage_ms(sz4_ctx* ctx, float* stage_ms, int n);
 
 /* Enable (1) or disable (0) per-stage event timing (default off). */

@@ -24,6 +24,9 @@ ShortChainsGreedy = 3   # smallz4.h:77
 ShortChainsLazy = 6     # smallz4.h:79
 MaxChainLength = 65535  # smallz4.h:115 ("-9")
 
+# per-stage device timings reported by sz4_last_stage_ms (include/smallz4_amd.h)
+STAGES = ("runs", "sort", "find_sorted", "find_long", "parse", "assemble")
+
 HEADERS = {"smallz4": _native.SZ4_HEADER_SMALLZ4, "independent": _native.SZ4_HEADER_INDEPENDENT,
            "none": _native.SZ4_HEADER_NONE}
 
@@ -134,9 +137,9 @@ class Compressor:
         self._lib.sz4_set_timing(self._h, int(on))
 
     def last_stage_ms(self) -> dict:
-        arr = (ctypes.c_float * 5)()
-        self._lib.sz4_last_stage_ms(self._h, arr, 5)
-        return dict(zip(["runs", "sort", "find", "parse", "assemble"], list(arr)))
+        arr = (ctypes.c_float * len(STAGES))()
+        self._lib.sz4_last_stage_ms(self._h, arr, len(STAGES))
+        return dict(zip(STAGES, list(arr)))
 
 
 _default = None

@@ -81,8 +81,8 @@ struct sz4_ctx {
   int device = 0;
   std::string err;
   bool timing = false;
-  hipEvent_t ev[6] = {};
-  float stageMs[5] = {};
+  hipEvent_t ev[kStages + 1] = {};
+  float stageMs[kStages] = {};
   uint32_t lastBlocks = 0;
   int stopAfter = 0;
   uint32_t lastChain = 0;
@@ -220,27 +220,32 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   mark(c, 0, s);
   launch_runs(in, dB, nb, dIv, dIvN, s);
   mark(c, 1, s);
-  if (maxChain > 0) launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
-  mark(c, 2, s);
   if (maxChain > 0) {
+    launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
     // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
-    if (maxChain > 0 && (e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)))
+    if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)))
       return c->fail(SZ4_E_DEVICE, "clear matches", e);
-    launch_find(in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
   }
+  mark(c, 2, s);
+  if (maxChain > 0)
+    launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
   mark(c, 3, s);
+  if (maxChain > 0)
+    launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
+  mark(c, 4, s);
   if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
                c->segState.as<uint4>(), c->status.as<int>(), s);
-  mark(c, 4, s);
+  mark(c, 5, s);
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   // optimal levels tokenize the parse's choices, greedy/lazy levels the (skip-filtered) matches
   const uint32_t* chosen = maxChain > (uint32_t)kGreedyMax ? c->sel.as<uint32_t>() : c->mlen.as<uint32_t>();
   launch_emit(in, dB, nb, maxChain, chosen, c->mdist.as<uint16_t>(), 0, c->tokens.as<Token>(),
               c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen, s);
-  mark(c, 5, s);
+  mark(c, 6, s);
   if ((e = hipGetLastError())) return c->fail(SZ4_E_DEVICE, "kernel launch", e);
 
   uint64_t total = 0;
@@ -256,7 +261,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if (endMark && (e = hipMemsetAsync(out + hdrLen + total, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "end mark", e);
   if ((e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "finish", e);
   if (c->timing)
-    for (int i = 0; i < 5; i++) hipEventElapsedTime(&c->stageMs[i], c->ev[i], c->ev[i + 1]);
+    for (int i = 0; i < kStages; i++) hipEventElapsedTime(&c->stageMs[i], c->ev[i], c->ev[i + 1]);
   c->lastBlocks = nb;
   *outSize = size;
   return SZ4_OK;
@@ -455,9 +460,9 @@ int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const vo
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)
 {
   if (!c || !stage_ms) return SZ4_E_ARG;
-  const int k = std::min(n, 5);
+  const int k = std::min(n, kStages);
   for (int i = 0; i < k; i++) stage_ms[i] = c->stageMs[i];
-  return 5;
+  return kStages;
 }
 
 void sz4_set_timing(sz4_ctx* c, int on)

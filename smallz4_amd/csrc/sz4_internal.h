@@ -18,6 +18,7 @@ constexpr int kLazyMax = 6;              // ShortChainsLazy
 constexpr uint32_t kHashMul = 48271;     // getHash32 multiplier
 constexpr int kHashBits = 20;
 constexpr uint64_t kNone = ~0ull;
+constexpr int kStages = 6;  // runs, sort, find (sorted pass), find (long pass), parse, assemble
 
 // one LZ4 block (all positions absolute byte offsets in the staged input)
 struct Block {
@@ -76,7 +77,8 @@ void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Inter
 void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
                  uint32_t* rank, hipStream_t s);
-void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
+// pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals)
+void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, const uint2* compact,
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  bool ldsWindow, hipStream_t s);

@@ -1718,7 +1718,7 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
 
 uint32_t find_lds_bytes() { return 65536 + 16; }
 
-void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
+void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
                  const uint32_t* ivCount, const uint2* compact, const uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
 {
@@ -1730,15 +1730,19 @@ void launch_find(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
       hipFuncSetAttribute((const void*)k_find_sorted<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       attr = true;
     }
-    hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                       compact, maxChain, mlen, mdist, matchBase);
-    hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                       compact, rank, maxChain, mlen, mdist, matchBase);
+    if (pass == 1)
+      hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
+                         ivCount, compact, maxChain, mlen, mdist, matchBase);
+    else
+      hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
+                         compact, rank, maxChain, mlen, mdist, matchBase);
   } else {
-    hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
-                       maxChain, mlen, mdist, matchBase);
-    hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
-                       maxChain, mlen, mdist, matchBase);
+    if (pass == 1)
+      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
+                         maxChain, mlen, mdist, matchBase);
+    else
+      hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
+                         maxChain, mlen, mdist, matchBase);
   }
 }
 
