@@ -88,11 +88,12 @@ struct sz4_ctx {
   uint32_t lastChain = 0;
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
-  DevBuf dpSegs, sel, reach, segState;
+  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState;
 
   std::vector<Block> hBlocks;
   std::vector<Segment> hSegs;
   std::vector<DpSeg> hDp;
+  std::vector<uint2> hWalk;
   uint64_t elemTotal = 0, rankTotal = 0, tokTotal = 0;
   bool ldsWindow = false;
   // plan cache for sz4_compress_blocks_device
@@ -143,6 +144,15 @@ void finish_plan(sz4_ctx* c)
   c->hSegs.clear();
   c->elemTotal = c->rankTotal = 0;
   for (uint32_t b = 0; b < c->hBlocks.size(); b++) add_segments(c, b);
+  // token-walk sub-segments: kWalkSeg positions each
+  c->hWalk.clear();
+  for (uint32_t b = 0; b < c->hBlocks.size(); b++) {
+    Block& B = c->hBlocks[b];
+    const uint64_t n = B.end - B.start;
+    B.walkFirst = (uint32_t)c->hWalk.size();
+    B.walkCount = (uint32_t)((n + kWalkSeg - 1) / kWalkSeg);
+    for (uint32_t k = 0; k < B.walkCount; k++) c->hWalk.push_back(make_uint2(b, k));
+  }
   // parse segments: positions [0, n - 6] of every block longer than 12 bytes, top segment first
   c->hDp.clear();
   for (uint32_t b = 0; b < c->hBlocks.size(); b++) {
@@ -188,7 +198,10 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->dpSegs.reserve(c->hDp.size() * sizeof(DpSeg) + 64)) ||
       (e = c->sel.reserve(stagedBytes * 4 + 64)) ||
       (e = c->reach.reserve(stagedBytes * 4 + 64)) ||
-      (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)))
+      (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
+      (e = c->walkSegs.reserve(c->hWalk.size() * sizeof(uint2) + 64)) ||
+      (e = c->walkSlots.reserve(c->hWalk.size() * 2 * kWalkCap * 4 + 64)) ||
+      (e = c->walkState.reserve(c->hWalk.size() * sizeof(uint4) + 64)))
     return c->fail(SZ4_E_NOMEM, "device allocation", e);
   return SZ4_OK;
 }
@@ -209,6 +222,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if ((e = hipMemcpyAsync(c->blocks.p, c->hBlocks.data(), nb * sizeof(Block), hipMemcpyHostToDevice, s)) ||
       (e = hipMemcpyAsync(c->segs.p, c->hSegs.data(), c->hSegs.size() * sizeof(Segment), hipMemcpyHostToDevice, s)) ||
       (e = hipMemcpyAsync(c->dpSegs.p, c->hDp.data(), c->hDp.size() * sizeof(DpSeg), hipMemcpyHostToDevice, s)) ||
+      (e = hipMemcpyAsync(c->walkSegs.p, c->hWalk.data(), c->hWalk.size() * sizeof(uint2), hipMemcpyHostToDevice, s)) ||
       (e = hipMemsetAsync(c->status.p, 0, 4, s)))
     return c->fail(SZ4_E_DEVICE, "upload plan", e);
   const uint32_t ns = (uint32_t)c->hSegs.size();
@@ -243,7 +257,9 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   // optimal levels tokenize the parse's choices, greedy/lazy levels the (skip-filtered) matches
   const uint32_t* chosen = maxChain > (uint32_t)kGreedyMax ? c->sel.as<uint32_t>() : c->mlen.as<uint32_t>();
-  launch_emit(in, dB, nb, maxChain, chosen, c->mdist.as<uint16_t>(), 0, c->tokens.as<Token>(),
+  // the parse's reach array is free by now: it holds each block's concatenated match positions
+  launch_emit(in, dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), maxChain, chosen, c->mdist.as<uint16_t>(), 0,
+              c->walkSlots.as<uint32_t>(), c->walkState.as<uint4>(), c->reach.as<uint32_t>(), c->tokens.as<Token>(),
               c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen, s);
   mark(c, 6, s);
   if ((e = hipGetLastError())) return c->fail(SZ4_E_DEVICE, "kernel launch", e);
@@ -297,7 +313,7 @@ void sz4_destroy(sz4_ctx* c)
   hipSetDevice(c->device);
   for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
                     &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
-                    &c->sel, &c->reach, &c->segState})
+                    &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState})
     b->release();
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);

@@ -30,6 +30,8 @@ struct Block {
   uint32_t flags;          // kBlk* below
   uint32_t dpFirst;        // first DpSeg of this block (top segment first)
   uint32_t dpCount;        // number of DpSegs (0 when the block is too short to parse)
+  uint32_t walkFirst;      // first token-walk sub-segment of this block
+  uint32_t walkCount;      // number of token-walk sub-segments (ceil(n / kWalkSeg))
 };
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kBlkLegacy = 1;         // always emitted compressed (legacy frame)
@@ -64,6 +66,12 @@ struct DpSeg {
 constexpr uint32_t kDpSeg = 16384;
 constexpr uint32_t kMaxDpSegs = 512;  // 8 MiB legacy block / kDpSeg
 
+// the token walk runs as sub-segments of kWalkSeg positions, each walked speculatively from its
+// first position and repaired by k_walk_fix; a sub-segment's match positions live in 2 * kWalkCap
+// u32 slots (speculative ones from kWalkCap on, repaired ones prepended below them)
+constexpr uint32_t kWalkSeg = 4096;
+constexpr uint32_t kWalkCap = kWalkSeg / 4 + 2;
+
 // one LZ4 sequence: literal run [litFrom, litFrom+lits) (block-relative) then a match
 struct Token {
   uint32_t litFrom, lits, mlen, dist;  // dist: low 16 bits; kTokLast marks the final literals-only token
@@ -86,8 +94,9 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, int* status,
                   hipStream_t s);
-void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
-                 const uint16_t* mdist, uint64_t matchBase, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
+void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
+                 uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
+                 uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
                  uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s);
 
 }  // namespace sz4

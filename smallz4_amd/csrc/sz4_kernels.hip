@@ -1501,12 +1501,149 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
 }
 
 // ================================================================================================
-// k_tokens: one wavefront per block walks the parse forward exactly like selectBestMatches
-// (smallz4.h:259-371) and records one token per (literal run, match): 16 bytes each.  The walk
-// keeps the current and the next 64-position window of chosen lengths in registers and jumps over
-// literal stretches with one ballot.  It also sizes the encoding and makes the stored/compressed
-// decision of smallz4.h:764-771.
+// Sequences.  The reference walks the parse forward (selectBestMatches, smallz4.h:259-371): a
+// position with a chosen length > 1 starts a match, others are literals.  The walk is split into
+// sub-segments of kWalkSeg positions walked at once (k_walk), repaired where a speculative start
+// was wrong (k_walk_fix), and turned into 16-byte tokens (literal run, match) by k_emit_tokens.
 // ================================================================================================
+
+constexpr int kWalkWaves = 4;  // sub-segments per k_walk workgroup
+
+// k_walk: one wavefront per sub-segment walks the parse forward from the sub-segment's first
+// position as if a sequence started there, and records the positions of the matches it takes
+// until the walk reaches the next sub-segment.  Four 64-position windows of chosen lengths sit in
+// registers (loads run three windows ahead); literal stretches are skipped with one ballot.
+__global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restrict__ blocks,
+                                                          const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                          const uint32_t* __restrict__ chosen, uint64_t matchBase,
+                                                          uint32_t* __restrict__ slotsAll, uint4* __restrict__ state)
+{
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  const uint32_t* L = chosen + (B.start - matchBase);
+  uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap) + kWalkCap;
+  const uint32_t a = ws.y * kWalkSeg;
+  const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+
+  uint32_t pos = a, wbase = a, m = 0;
+  bool viaMatch = false;
+  uint32_t wL, xL1, xL2, xL3;
+  auto ldw = [&](uint32_t b) -> uint32_t { return b + lane < n ? L[b + lane] : 0u; };
+  wL = ldw(a);
+  xL1 = ldw(a + 64);
+  xL2 = ldw(a + 128);
+  xL3 = ldw(a + 192);
+  while (pos < aNext) {
+    while (pos >= wbase + 64) {
+      if (pos < wbase + 256) {
+        wbase += 64;
+        wL = xL1;
+        xL1 = xL2;
+        xL2 = xL3;
+        xL3 = ldw(wbase + 192);
+      } else {
+        wbase = pos & ~63u;
+        wL = ldw(wbase);
+        xL1 = ldw(wbase + 64);
+        xL2 = ldw(wbase + 128);
+        xL3 = ldw(wbase + 192);
+      }
+    }
+    const uint32_t rel = pos - wbase;
+    const uint64_t mm = __ballot(wL > 1u) & (~0ull << rel);
+    const uint32_t q = mm ? wbase + (uint32_t)__builtin_ctzll(mm) : wbase + 64;  // next match (or window end)
+    if (q >= aNext) {
+      viaMatch = false;  // literals carry the path to aNext itself
+      break;
+    }
+    if (mm == 0) {
+      pos = q;
+      viaMatch = false;
+      continue;
+    }
+    if (lane == 0) slots[m] = q;
+    m++;
+    pos = q + rdlane(wL, q - wbase);
+    viaMatch = true;
+  }
+  if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, viaMatch ? pos : aNext, 0u);
+}
+
+// k_walk_fix: one wavefront per block.  Sub-segment k's walk is exact when the true path enters it
+// at a position the speculative walk also visits; otherwise the path is walked again from its true
+// entry until it meets the speculative path, and the repaired matches go in front of the
+// speculative matches that survive.
+__global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ chosen,
+                                                 uint64_t matchBase, uint32_t* __restrict__ slotsAll,
+                                                 uint4* __restrict__ state)
+{
+  __shared__ uint32_t fix[kWalkCap];
+  const Block B = blocks[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  const uint32_t* L = chosen + (B.start - matchBase);
+  for (uint32_t k = 1; k < B.walkCount; k++) {
+    const uint32_t idx = B.walkFirst + k;
+    const uint32_t entry = state[idx - 1].z;  // exact exit of the sub-segment before
+    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+    const uint4 st = state[idx];
+    if (entry == a) continue;
+    uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+    const uint32_t m = st.y - kWalkCap;
+    if (entry >= aNext) {
+      if (lane == 0) state[idx] = make_uint4(st.y, st.y, entry, 0u);
+      continue;
+    }
+    // i = first speculative match at or after p (wave-parallel over 64 slots at a time)
+    auto first_at = [&](uint32_t from, uint32_t p) -> uint32_t {
+      for (uint32_t b = from; b < m; b += 64) {
+        const uint64_t ge = __ballot(b + lane < m && slots[kWalkCap + b + lane] >= p);
+        if (ge) return b + (uint32_t)__builtin_ctzll(ge);
+      }
+      return m;
+    };
+    // q lies strictly inside speculative match i - 1
+    auto inside = [&](uint32_t i, uint32_t q) -> bool {
+      if (i == 0) return false;
+      const uint32_t pj = slots[kWalkCap + i - 1];
+      return pj + L[pj] > q;
+    };
+    uint32_t i = first_at(0, entry);
+    if (!inside(i, entry)) {
+      if (lane == 0) state[idx] = make_uint4(kWalkCap + i, st.y, st.z, 0u);
+      continue;
+    }
+    uint32_t q = entry, f = 0;
+    bool merged = false;
+    while (q < aNext) {
+      const uint32_t lq = L[q];
+      if (lq > 1u) {
+        if (lane == 0) fix[f] = q;
+        f++;
+        q += lq;
+      } else {
+        q++;
+      }
+      i = first_at(i, q);
+      if (q < aNext && !inside(i, q)) {
+        merged = true;
+        break;
+      }
+    }
+    __syncthreads();
+    const uint32_t iMerge = merged ? i : m;
+    const uint32_t start = kWalkCap + iMerge - f;
+    for (uint32_t t = lane; t < f; t += 64) slots[start + t] = fix[t];
+    if (lane == 0) state[idx] = make_uint4(start, st.y, merged ? st.z : q, 0u);
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ uint64_t token_bytes(uint64_t lits, uint32_t mlen, bool last)
 {
   uint64_t b = 1 + lits + (lits >= 15 ? (lits - 15) / 255 + 1 : 0);
@@ -1517,70 +1654,69 @@ __device__ __forceinline__ uint64_t token_bytes(uint64_t lits, uint32_t mlen, bo
   return b;
 }
 
-__global__ __launch_bounds__(64) void k_tokens(const Block* __restrict__ blocks, uint32_t maxChain,
-                                               const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
-                                               uint64_t matchBase, Token* __restrict__ tokAll, uint32_t* __restrict__ ntokOut,
-                                               uint32_t* __restrict__ blockBytes)
+// k_emit_tokens: one 256-thread workgroup per block concatenates its sub-segments' match lists,
+// turns consecutive matches into sequences (literal run before each match, smallz4.h:259-371),
+// sizes the encoding and makes the stored/compressed decision of smallz4.h:764-771.
+__global__ __launch_bounds__(256) void k_emit_tokens(const Block* __restrict__ blocks, uint32_t maxChain,
+                                                     const uint32_t* __restrict__ chosen,
+                                                     const uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                                     const uint32_t* __restrict__ slotsAll,
+                                                     const uint4* __restrict__ state, uint32_t* __restrict__ posAll,
+                                                     Token* __restrict__ tokAll, uint32_t* __restrict__ ntokOut,
+                                                     uint32_t* __restrict__ blockBytes)
 {
+  __shared__ uint64_t s_red[4];
+  __shared__ uint32_t s_pre[4];
   const Block B = blocks[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint64_t n = B.end - B.start;
-  const uint32_t* L = mlen + (B.start - matchBase);
-  const uint16_t* D = mdist + (B.start - matchBase);
-  Token* tok = tokAll + B.tokOff;
   const bool stored = maxChain == 0;
   const bool legacy = (B.flags & kBlkLegacy) != 0;
   uint64_t enc = 0;
   uint32_t ntok = 0;
   if (!stored) {
-    uint64_t pos = 0, litFrom = 0, lits = 0;
-    uint64_t wbase = 0;
-    uint32_t wL = lane < n ? L[lane] : 0u, wD = lane < n ? D[lane] : 0u;
-    uint32_t nL = 64 + lane < n ? L[64 + lane] : 0u, nD = 64 + lane < n ? D[64 + lane] : 0u;
-    while (pos < n) {
-      if (pos >= wbase + 64) {
-        if (pos < wbase + 128) {
-          wbase += 64;
-          wL = nL;
-          wD = nD;
-        } else {
-          wbase = pos & ~63ull;
-          wL = wbase + lane < n ? L[wbase + lane] : 0u;
-          wD = wbase + lane < n ? D[wbase + lane] : 0u;
-        }
-        const uint64_t nb = wbase + 64 + lane;
-        nL = nb < n ? L[nb] : 0u;
-        nD = nb < n ? D[nb] : 0u;
-      }
-      const uint32_t rel = (uint32_t)(pos - wbase);
-      const uint64_t mm = __ballot(wL > 1u) & (~0ull << rel);
-      if (mm == 0) {
-        const uint64_t end = wbase + 64 < n ? wbase + 64 : n;
-        if (lits == 0) litFrom = pos;
-        lits += end - pos;
-        pos = end;
-        continue;
-      }
-      const uint32_t f = (uint32_t)__builtin_ctzll(mm);
-      if (f > rel) {
-        if (lits == 0) litFrom = pos;
-        lits += f - rel;
-      }
-      const uint32_t Lm = rdlane(wL, f), Dm = rdlane(wD, f);
-      if (lane == 0) tok[ntok] = Token{(uint32_t)(lits ? litFrom : 0), (uint32_t)lits, Lm, Dm};
-      ntok++;
-      enc += token_bytes(lits, Lm, false);
-      lits = 0;
-      pos = wbase + f + Lm;
+    const uint32_t* L = chosen + (B.start - matchBase);
+    const uint16_t* D = mdist + (B.start - matchBase);
+    uint32_t* posList = posAll + (B.start - matchBase);
+    Token* tok = tokAll + B.tokOff;
+    // 1. concatenate the sub-segments' match positions
+    uint32_t M = 0;
+    for (uint32_t k = 0; k < B.walkCount; k++) {
+      const uint32_t idx = B.walkFirst + k;
+      const uint4 st = state[idx];
+      const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+      for (uint32_t t = tid; t < st.y - st.x; t += 256) posList[M + t] = slots[st.x + t];
+      M += st.y - st.x;
     }
-    // the block always ends with literals (the last five positions are never matched)
-    if (lane == 0) tok[ntok] = Token{(uint32_t)litFrom, (uint32_t)lits, 0u, kTokLast};
-    ntok++;
-    enc += token_bytes(lits, 0, true);
+    __syncthreads();
+    // 2. one sequence per match (literals before it), then the closing literal run
+    for (uint32_t t = tid; t <= M; t += 256) {
+      uint32_t prevEnd = 0;
+      if (t > 0) {
+        const uint32_t pp = posList[t - 1];
+        prevEnd = pp + L[pp];
+      }
+      if (t < M) {
+        const uint32_t p = posList[t], lits = p - prevEnd, Lm = L[p];
+        tok[t] = Token{lits ? prevEnd : 0u, lits, Lm, (uint32_t)D[p]};
+        enc += token_bytes(lits, Lm, false);
+      } else {
+        tok[t] = Token{prevEnd, (uint32_t)(n - prevEnd), 0u, kTokLast};
+        enc += token_bytes(n - prevEnd, 0, true);
+      }
+    }
+    // workgroup sum of the encoded size
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) enc += __shfl_xor(enc, d, 64);
+    if (lane == 0) s_red[wave] = enc;
+    __syncthreads();
+    enc = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    ntok = M + 1;
   }
+  (void)s_pre;
   const bool useEnc = (enc < n && !stored) || legacy;
   const uint32_t bytes = (uint32_t)(useEnc ? enc : n);
-  if (lane == 0) {
+  if (tid == 0) {
     ntokOut[blockIdx.x] = useEnc ? ntok : 0u;
     blockBytes[blockIdx.x] = (useEnc ? 0u : 0x80000000u) | (bytes + 4u);
   }
@@ -1760,12 +1896,19 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
                      segState);
 }
 
-void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, const uint32_t* mlen,
-                 const uint16_t* mdist, uint64_t matchBase, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
+void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
+                 uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
+                 uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
                  uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s)
 {
   if (!nblocks) return;
-  hipLaunchKernelGGL(k_tokens, dim3(nblocks), dim3(64), 0, s, blocks, maxChain, mlen, mdist, matchBase, tokens, ntok, blockBytes);
+  if (maxChain > 0 && nwalk) {
+    hipLaunchKernelGGL(k_walk, dim3((nwalk + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs,
+                       nwalk, chosen, matchBase, walkSlots, walkState);
+    hipLaunchKernelGGL(k_walk_fix, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState);
+  }
+  hipLaunchKernelGGL(k_emit_tokens, dim3(nblocks), dim3(256), 0, s, blocks, maxChain, chosen, mdist, matchBase, walkSlots,
+                     walkState, posList, tokens, ntok, blockBytes);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, blockBytes, nblocks, offsets);
   hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(256), 0, s, in, blocks, tokens, ntok, blockBytes, offsets, out, headerLen);
 }
