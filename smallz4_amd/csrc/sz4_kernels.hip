@@ -725,16 +725,18 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
         }
         qn = 0;
       };
-      // one candidate for this lane: slot cs with first 12 bytes k0..k2
+      // lanes whose match can still grow past 12 bytes
+      const uint64_t satOk = __ballot(limit > 12u);
+      // one candidate for this lane: slot cs with first 12 bytes k0..k2.  The common prefix is
+      // 4 + (trailing zero bits of x2:x1) / 8; a candidate from another hash group never has x0 = 0
       auto visit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
         const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
-        const uint32_t f1 = min((uint32_t)(__ffs(x1) - 1) >> 3, 4u);
-        const uint32_t f2 = min((uint32_t)(__ffs(x2) - 1) >> 3, 4u);
-        uint32_t lcp = 4u + f1 + (f1 == 4u ? f2 : 0u);
-        lcp = lcp < cap12 ? lcp : cap12;
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);  // ~0u when zero
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        const uint32_t lcp = min(4u + (z >> 3), cap12);
         const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
         bestKey = key > bestKey ? key : bestKey;
-        const uint64_t sat = __ballot(mine && x0 == 0u && lcp == 12u && limit > 12u);
+        const uint64_t sat = __ballot(mine && (x0 | x1 | x2) == 0u) & satOk;
         if (sat) {
           const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
@@ -777,12 +779,19 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
           const uint64_t fp = S.w0 + fRel;
           const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
-          for (int32_t k = 0; k < n; k++) {
+          if (needWin) {
+            for (int32_t k = 0; k < n; k++) {
+              if (run && rdlane(fRel, k) < lbRel) run = false;
+              visit(run, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+            }
+          } else {
+            // no window test: every lane may take the candidate (only the group's lanes can match)
+            for (int32_t k = 0; k < n; k++) {
 #if SZ4_DIAG == 3
-            dB++;
+              dB++;
 #endif
-            if (needWin && run && rdlane(fRel, k) < lbRel) run = false;
-            visit(run, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              visit(true, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+            }
           }
           cBase -= 64;
         }
