@@ -535,7 +535,8 @@ __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t 
 // improvement, step limit).  Prefixes are capped at kLongCap: a target reaching it keeps the marker
 // kLongMatch and is finished by k_find (pass 2), which walks long repeats in text order.
 // ================================================================================================
-constexpr uint32_t kLongCap = 32;
+constexpr uint32_t kLongCap = 32;    // bounded chains: prefixes >= this are finished by pass 2
+constexpr uint32_t kLongCap9 = 256;  // -9: pass 1 extends exactly up to this
 constexpr uint32_t kSatQ = 128;  // saturated-candidate queue per wavefront (flushed at 64)
 // broadcast chunk list: >= slots / 64 + number of groups of >= 64 slots (64 Ki slots with the LDS
 // window, 128 Ki otherwise)
@@ -643,7 +644,8 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
       uint64_t lb = p > kWindow ? p - kWindow : 0;
       if (cut != kNone && ref_hash(me0) == cutHash && cut > lb) lb = cut;
       lbRel = lb > S.w0 ? (uint32_t)(lb - S.w0) : 0u;
-      limit = room < kLongCap ? room : kLongCap;
+      const uint32_t cap = unlimited ? kLongCap9 : kLongCap;
+      limit = room < cap ? room : cap;
     }
     uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
     bool isLong = false, run = active && bestLen < room && gs < slot;
