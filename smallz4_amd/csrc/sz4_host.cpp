@@ -162,8 +162,10 @@ void finish_plan(sz4_ctx* c)
     B.dpCount = 0;
     if (n <= (uint64_t)kTailNoMatch) continue;
     const uint64_t top = n - 1 - kTailLiterals;
-    for (uint64_t hi = top, k = 0;; hi -= kDpSeg, k++) {
-      const uint64_t lo = hi + 1 >= kDpSeg ? hi + 1 - kDpSeg : 0;
+    const uint64_t seg = dp_segment_size(n);
+    B.dpSize = (uint32_t)seg;
+    for (uint64_t hi = top, k = 0;; hi -= seg, k++) {
+      const uint64_t lo = hi + 1 >= seg ? hi + 1 - seg : 0;
       c->hDp.push_back(DpSeg{b, (uint32_t)k, (uint32_t)lo, (uint32_t)hi});
       B.dpCount++;
       if (lo == 0) break;

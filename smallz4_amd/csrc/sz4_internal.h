@@ -32,6 +32,8 @@ struct Block {
   uint32_t dpCount;        // number of DpSegs (0 when the block is too short to parse)
   uint32_t walkFirst;      // first token-walk sub-segment of this block
   uint32_t walkCount;      // number of token-walk sub-segments (ceil(n / kWalkSeg))
+  uint32_t dpSize;         // positions per parse segment (dp_segment_size(n))
+  uint32_t pad;
 };
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
 constexpr uint32_t kBlkLegacy = 1;         // always emitted compressed (legacy frame)
@@ -55,7 +57,7 @@ struct Interval {
 // block b owns iv[b * kMaxIv .. b * kMaxIv + ivCount[b])
 constexpr uint32_t kMaxIv = 136;  // > 8 MiB / 65300
 
-// the optimal parse of one block runs as independent segments of kDpSeg positions (top segment
+// the optimal parse of one block runs as independent segments of B.dpSize positions (top segment
 // first, k = 0): every segment is parsed at once from a guessed boundary, then k_dp_fix walks the
 // boundaries top-down and re-parses each segment until it agrees with the speculative parse.
 struct DpSeg {
@@ -63,8 +65,10 @@ struct DpSeg {
   uint32_t k;              // 0 = the segment holding the block's last parsed position
   uint32_t lo, hi;         // block-relative positions [lo, hi], parsed from hi down
 };
-constexpr uint32_t kDpSeg = 16384;
-constexpr uint32_t kMaxDpSegs = 512;  // 8 MiB legacy block / kDpSeg
+// short segments give more parallelism; the repair pass walks a block's boundaries one after the
+// other, so large blocks keep longer segments
+inline uint32_t dp_segment_size(uint64_t n) { return n <= 65536 ? 4096u : 16384u; }
+constexpr uint32_t kMaxDpSegs = 512;  // 8 MiB legacy block / 16384
 
 // the token walk runs as sub-segments of kWalkSeg positions, each walked speculatively from its
 // first position and repaired by k_walk_fix; a sub-segment's match positions live in 2 * kWalkCap

@@ -1130,7 +1130,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
 //   k_prep    one wavefront per block: clears the positions the reference never searched and, at
 //             greedy/lazy levels, replays the reference's skip scan (smallz4.h:726-744);
 //   k_dp_spec one wavefront per DpSeg: the backward optimal parse (estimateCosts,
-//             smallz4.h:376-472) of kDpSeg positions.  The top segment of a block starts from the
+//             smallz4.h:376-472) of B.dpSize positions.  The top segment of a block starts from the
 //             block end exactly; every other segment starts from a guessed boundary (costs 0 above
 //             it).  Also writes reach[i] = max(q + len[q]) over the segment's positions q < i.
 //   k_dp_fix  one wavefront per block: walks the segment boundaries top-down.  Segment k is parsed
@@ -1414,7 +1414,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   // exact cost of a position above the segment being repaired (0 past the parsed range)
   auto exact_above = [&](uint32_t j) -> uint32_t {
     if (j > first) return 0u;
-    const uint32_t k = (first - j) / kDpSeg;
+    const uint32_t k = (first - j) / B.dpSize;
     const uint32_t v = ld_fresh(&cost[j]);
     return j < convTab[k] ? v + deltaTab[k] : v;
   };
