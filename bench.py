@@ -29,8 +29,21 @@ from concurrent.futures import ThreadPoolExecutor
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from smallz4_amd import synth  # noqa: E402  (input generators; the HIP library loads lazily)
+
 METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "r01c_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
+
+# input shapes (smallz4_amd/synth.py); the default is the headline workload (configs[1])
+DATA = {
+    "enwik8": ("synthetic enwik8-shaped text (smallz4_amd/synth.py; enwik8 is not available offline)",
+               lambda n, seed: synth.enwik8_like(n, seed=seed)),
+    "zeros_urandom": ("synthetic: alternating 128 KiB runs of zeros and urandom bytes (configs[4]'s two extremes)",
+                      lambda n, seed: synth.zeros_urandom(n, seed=seed)),
+    "zeros": ("synthetic: all zero bytes", lambda n, seed: bytes(n)),
+    "random": ("synthetic: urandom bytes (numpy, seeded)", lambda n, seed: synth.random_bytes(n, seed=seed)),
+}
 
 
 def parse_args():
@@ -44,6 +57,8 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--verify-threads", type=int, default=16)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--data", default="enwik8", choices=sorted(DATA),
+                    help="synthetic input shape (enwik8: configs[1]; zeros_urandom: configs[4])")
     return ap.parse_args()
 
 
@@ -108,11 +123,10 @@ def main():
         torch.cuda.set_device(local)
 
     import smallz4_amd
-    from smallz4_amd import synth
 
     chain = smallz4_amd.level_to_chain(args.level)
     nbytes = int(args.mb * 1e6)
-    data = synth.enwik8_like(nbytes, seed=8 + rank)
+    data = DATA[args.data][1](nbytes, 8 + rank)
     t_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda(local)
     comp = smallz4_amd.Compressor(device=local)
     cap = comp._lib.sz4_bound(nbytes, args.block_size)
@@ -170,9 +184,9 @@ def main():
         alg_bytes = nbytes + 4 * nbytes + 6 * targets
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "r01_find_hbm_bytes.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
+        default_cfg = args.data == "enwik8" and args.block_size == 65536 and args.level == 9 and nbytes == 100_000_000
+        if default_cfg and os.path.exists(PMC_FILE):
+            with open(PMC_FILE) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         rec = {
             "metric": METRIC,
@@ -186,8 +200,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic enwik8-shaped text (smallz4_amd/synth.py; enwik8 is not available offline)",
-            "config": {"workload": f"enwik8-shaped {args.mb:g} MB per GPU as independent {args.block_size}-byte "
+            "data": DATA[args.data][0],
+            "config": {"workload": f"{args.data}-shaped {args.mb:g} MB per GPU as independent {args.block_size}-byte "
                                    f"blocks, level -{args.level} (maxChainLength {chain})",
                        "block_size": args.block_size, "level": args.level, "bytes_per_gpu": nbytes,
                        "parallelism": f"blocks sharded over {world} GPU(s), no data-path collective"},

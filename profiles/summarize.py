@@ -1,0 +1,124 @@
+#!/usr/bin/env python3
+"""Summarise one profiles/collect.sh run (gpurun_out/<tag>/) into profiles/<tag>_*.
+
+    python profiles/summarize.py r01c [--src gpurun_out]
+
+Writes
+  <tag>_kernel_stats.csv   the rocprofv3 --kernel-trace --stats table, as collected
+  <tag>_kernel_stats.md    per kernel: calls, average duration, share, and the PMC passes
+                           (FETCH_SIZE x2, WRITE_SIZE, SQ issue counters) averaged per launch
+  <tag>_find_hbm_bytes.json  k_find_sorted's HBM bytes per launch (bench.py reads this file
+                           for the roofline "traffic" field)
+  <tag>_bench.json         the bench.py JSON line of the same run
+
+FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950 tallies 128-B requests at 64 B);
+WRITE_SIZE is taken as reported.  Both are kilobytes per dispatch in rocprofv3's CSV.
+"""
+from __future__ import annotations
+
+import argparse
+import csv
+import json
+import os
+import re
+import shutil
+from collections import defaultdict
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def short(name: str) -> str:
+    name = re.sub(r"\(.*$", "", name)
+    return name.replace("void ", "").strip()
+
+
+def pmc(path: str):
+    """kernel -> counter -> (sum, launches)"""
+    acc = defaultdict(lambda: defaultdict(lambda: [0.0, set()]))
+    if not os.path.exists(path):
+        return acc
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            k = short(row["Kernel_Name"])
+            if not k.startswith("sz4::"):
+                continue
+            a = acc[k][row["Counter_Name"]]
+            a[0] += float(row["Counter_Value"])
+            a[1].add(row["Dispatch_Id"])
+    return acc
+
+
+def per_launch(acc, k, c):
+    v = acc.get(k, {}).get(c)
+    if not v or not v[1]:
+        return None
+    return v[0] / len(v[1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    a = ap.parse_args()
+    src = os.path.join(a.src, a.tag)
+    stats = os.path.join(src, "trace", "bench_kernel_stats.csv")
+    rows = []
+    with open(stats) as f:
+        for r in csv.DictReader(f):
+            if short(r["Name"]).startswith("sz4::"):
+                rows.append(r)
+    shutil.copy(stats, os.path.join(HERE, f"{a.tag}_kernel_stats.csv"))
+    fetch = pmc(os.path.join(src, "fetch", "bench_counter_collection.csv"))
+    write = pmc(os.path.join(src, "write", "bench_counter_collection.csv"))
+    sq = pmc(os.path.join(src, "sq", "bench_counter_collection.csv"))
+
+    def fmt(v, scale=1.0, p=1):
+        return "-" if v is None else (f"{v * scale:.{p}f}" if scale != "e" else f"{v:.3g}")
+
+    lines = [f"# {a.tag} kernel profile (bench.py default workload: 100 MB, 64 KiB blocks, -9)", "",
+             f"Source: `bash profiles/collect.sh {a.tag}` on one MI355X, summarised by "
+             f"`python profiles/summarize.py {a.tag}` (rocprofv3 --kernel-trace --stats; every PMC pass separate).",
+             "FETCH_SIZE doubled per MI355X_MICROARCH.md; MB = 1e6 bytes per launch.", "",
+             "| kernel | calls | avg us | % | FETCH x2 (MB) | WRITE (MB) | VALU instr | SALU instr | LDS instr | wait-any % |",
+             "|---|---|---|---|---|---|---|---|---|---|"]
+    find = None
+    for r in rows:
+        k = short(r["Name"])
+        fe = per_launch(fetch, k, "FETCH_SIZE")
+        wr = per_launch(write, k, "WRITE_SIZE")
+        valu = per_launch(sq, k, "SQ_INSTS_VALU")
+        salu = per_launch(sq, k, "SQ_INSTS_SALU")
+        lds = per_launch(sq, k, "SQ_INSTS_LDS")
+        wc = per_launch(sq, k, "SQ_WAVE_CYCLES")
+        wa = per_launch(sq, k, "SQ_WAIT_ANY")
+        wait = None if not wc or wa is None else 100.0 * wa / wc
+        lines.append(f"| {k} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} | "
+                     f"{fmt(fe, 2 * 1024 / 1e6)} | {fmt(wr, 1024 / 1e6)} | {fmt(valu, 'e')} | {fmt(salu, 'e')} | "
+                     f"{fmt(lds, 'e')} | {fmt(wait, 1.0, 0)} |")
+        if k.startswith("sz4::k_find_sorted"):
+            find = (k, float(r["AverageNs"]), fe, wr)
+    with open(os.path.join(HERE, f"{a.tag}_kernel_stats.md"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    bench = os.path.join(src, "bench.json")
+    if os.path.exists(bench):
+        shutil.copy(bench, os.path.join(HERE, f"{a.tag}_bench.json"))
+    if find:
+        k, avg_ns, fe, wr = find
+        fb = None if fe is None else int(round(fe * 1024 * 2))
+        wb = None if wr is None else int(round(wr * 1024))
+        out = {"kernel": "k_find_sorted", "tag": a.tag,
+               "workload": "bench.py default: 100 MB enwik8-shaped, 64 KiB blocks, -9",
+               "avg_duration_us": round(avg_ns / 1e3, 1),
+               "fetch_bytes_corrected": fb, "write_bytes": wb,
+               "hbm_bytes_per_launch": None if fb is None or wb is None else fb + wb,
+               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (profiles/collect.sh); "
+                         "FETCH_SIZE doubled per MI355X_MICROARCH.md; WRITE_SIZE as reported"}
+        with open(os.path.join(HERE, f"{a.tag}_find_hbm_bytes.json"), "w") as f:
+            json.dump(out, f, indent=1)
+            f.write("\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
