@@ -88,7 +88,7 @@ struct sz4_ctx {
   uint32_t lastChain = 0;
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
-  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState;
+  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
 
   std::vector<Block> hBlocks;
   std::vector<Segment> hSegs;
@@ -96,6 +96,7 @@ struct sz4_ctx {
   std::vector<uint2> hWalk;
   uint64_t elemTotal = 0, rankTotal = 0, tokTotal = 0;
   bool ldsWindow = false;
+  uint32_t hybridLds = 0;  // k_find_long9's LDS staging when the window is not LDS-resident
   // plan cache for sz4_compress_blocks_device
   uint64_t planN = ~0ull;
   uint32_t planBS = 0;
@@ -172,9 +173,12 @@ void finish_plan(sz4_ctx* c)
     }
   }
   c->ldsWindow = true;
+  c->hybridLds = 0;
   for (const Segment& S : c->hSegs) {
     const Block& B = c->hBlocks[S.block];
     if ((B.end - S.w0 + 8 + 3) / 4 * 4 > find_lds_bytes()) c->ldsWindow = false;
+    const uint64_t end = std::min<uint64_t>(S.s1 + 64, B.end + 8);
+    c->hybridLds = std::max<uint32_t>(c->hybridLds, (uint32_t)((end - S.w0 + 3) / 4 * 4));
   }
 }
 
@@ -203,7 +207,12 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
       (e = c->walkSegs.reserve(c->hWalk.size() * sizeof(uint2) + 64)) ||
       (e = c->walkSlots.reserve(c->hWalk.size() * 2 * kWalkCap * 4 + 64)) ||
-      (e = c->walkState.reserve(c->hWalk.size() * sizeof(uint4) + 64)))
+      (e = c->walkState.reserve(c->hWalk.size() * sizeof(uint4) + 64)) ||
+      (e = c->longFlag.reserve(nb * 4 + 64)) ||
+      (e = c->longBits.reserve(stagedBytes / 8 + 64)) ||
+      (e = c->segLong.reserve(c->hSegs.size() * 4 + 64)) ||
+      (e = c->rmqUp.reserve((stagedBytes + nb + 8) * 4)) ||
+      (e = c->rmqDown.reserve((stagedBytes + nb + 8) * 4)))
     return c->fail(SZ4_E_NOMEM, "device allocation", e);
   return SZ4_OK;
 }
@@ -225,7 +234,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
       (e = hipMemcpyAsync(c->segs.p, c->hSegs.data(), c->hSegs.size() * sizeof(Segment), hipMemcpyHostToDevice, s)) ||
       (e = hipMemcpyAsync(c->dpSegs.p, c->hDp.data(), c->hDp.size() * sizeof(DpSeg), hipMemcpyHostToDevice, s)) ||
       (e = hipMemcpyAsync(c->walkSegs.p, c->hWalk.data(), c->hWalk.size() * sizeof(uint2), hipMemcpyHostToDevice, s)) ||
-      (e = hipMemsetAsync(c->status.p, 0, 4, s)))
+      (e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
     return c->fail(SZ4_E_DEVICE, "upload plan", e);
   const uint32_t ns = (uint32_t)c->hSegs.size();
   Block* dB = c->blocks.as<Block>();
@@ -239,22 +248,26 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if (maxChain > 0) {
     launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
     // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
-    if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)))
+    if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
+        (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
       return c->fail(SZ4_E_DEVICE, "clear matches", e);
   }
   mark(c, 2, s);
   if (maxChain > 0)
-    launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
+    launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
+                nullptr, c->ldsWindow, c->hybridLds, s);
   mark(c, 3, s);
   if (maxChain > 0)
-    launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->ldsWindow, s);
+    launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
+                c->longFlag.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
   mark(c, 4, s);
   if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
-               c->segState.as<uint4>(), c->status.as<int>(), s);
+               c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp.as<uint32_t>(), c->rmqDown.as<uint32_t>(),
+               c->status.as<int>(), s);
   mark(c, 5, s);
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   // optimal levels tokenize the parse's choices, greedy/lazy levels the (skip-filtered) matches
@@ -315,7 +328,8 @@ void sz4_destroy(sz4_ctx* c)
   hipSetDevice(c->device);
   for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
                     &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
-                    &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState})
+                    &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState, &c->longFlag,
+                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong})
     b->release();
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);

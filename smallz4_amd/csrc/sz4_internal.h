@@ -84,20 +84,24 @@ constexpr uint32_t kTokLast = 0x80000000u;
 
 // kernels (sz4_kernels.hip)
 uint32_t find_lds_bytes();
+uint32_t find_hybrid_lds_max();  // LDS for k_find_long9's [w0, s1 + 64) staging when the block is larger
 void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount,
                  hipStream_t s);
 void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
                  uint32_t* rank, hipStream_t s);
 // pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals)
+// scratch: per-slot words free after k_sort (the skip pointers of k_find_long9); longBits: one bit per
+// position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
-                 const Interval* iv, const uint32_t* ivCount, const uint2* compact,
+                 const Interval* iv, const uint32_t* ivCount, const uint2* compact, uint2* scratch,
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
-                 bool ldsWindow, hipStream_t s);
+                 uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, bool ldsWindow, uint32_t hybridLds,
+                 hipStream_t s);
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
-                  uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, int* status,
-                  hipStream_t s);
+                  uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,
+                  const uint32_t* longFlag, uint32_t* rmqUp, uint32_t* rmqDown, int* status, hipStream_t s);
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
                  uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
                  uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,

@@ -15,8 +15,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "sz4_internal.h"
 
+#ifndef SZ4_SPEC_ATTR
+#define SZ4_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))  // 8 waves/SIMD (SGPR spills to lanes are cheap)
+#endif
 #ifndef SZ4_DIAG
 #define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
 #endif
@@ -315,6 +320,7 @@ __global__ __launch_bounds__(256) void k_runs(const uint8_t* __restrict__ in, co
 // ================================================================================================
 constexpr int kSortThreads = 1024;
 constexpr int kSortWaves = kSortThreads / 64;
+constexpr uint32_t kSortBatch = 8;  // loads in flight per lane in the latency-bound loops
 
 __device__ __forceinline__ uint32_t pos_bits(uint32_t W) { return W <= 65536u ? 16u : 17u; }
 __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
@@ -364,16 +370,27 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
   const uint32_t pb = pos_bits(W);
   const uint32_t posMask = (1u << pb) - 1u;
 
-  // 1. packed elements in position order (intervals compacted out)
-  for (uint32_t r = tid; r < W; r += kSortThreads) {
-    const uint64_t q = S.w0 + r;
-    uint32_t idx = r;
-    bool skip = false;
-    for (uint32_t j = 0; j < ne; j++) {
-      if (q >= exHi[j]) idx -= (uint32_t)(exHi[j] - exLo[j]);
-      else if (q >= exLo[j]) skip = true;
+  // 1. packed elements in position order (intervals compacted out); loads issued kSortBatch at a time
+  for (uint32_t r0 = tid; r0 < W; r0 += kSortThreads * kSortBatch) {
+    uint32_t key[kSortBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++) {
+      const uint32_t r = r0 + u * kSortThreads;
+      key[u] = r < W ? gload4(in, S.w0 + r) : 0u;
     }
-    if (!skip) src[idx] = (key_hash(gload4(in, q), pb) << pb) | r;
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++) {
+      const uint32_t r = r0 + u * kSortThreads;
+      if (r >= W) break;
+      const uint64_t q = S.w0 + r;
+      uint32_t idx = r;
+      bool skip = false;
+      for (uint32_t j = 0; j < ne; j++) {
+        if (q >= exHi[j]) idx -= (uint32_t)(exHi[j] - exLo[j]);
+        else if (q >= exLo[j]) skip = true;
+      }
+      if (!skip) src[idx] = (key_hash(key[u], pb) << pb) | r;
+    }
   }
   __syncthreads();
 
@@ -385,7 +402,14 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
     const uint32_t sh = pb + 8u * pass;
     for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
     __syncthreads();
-    for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&hist[wave][(src[i] >> sh) & 255u], 1u);
+    for (uint32_t i0 = b0 + lane; i0 < b1; i0 += 64 * kSortBatch) {
+      uint32_t v[kSortBatch];
+#pragma unroll
+      for (uint32_t u = 0; u < kSortBatch; u++) v[u] = i0 + 64 * u < b1 ? src[i0 + 64 * u] : 0u;
+#pragma unroll
+      for (uint32_t u = 0; u < kSortBatch; u++)
+        if (i0 + 64 * u < b1) atomicAdd(&hist[wave][(v[u] >> sh) & 255u], 1u);
+    }
     __syncthreads();
     uint32_t total = 0;
     if (tid < 256) {
@@ -405,22 +429,33 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
       for (int w = 0; w < kSortWaves; w++) hist[w][tid] += base;
     }
     __syncthreads();
-    for (uint32_t base = b0; base < b1; base += 64) {
-      const uint32_t i = base + lane;
-      const bool valid = i < b1;
-      const uint32_t e = valid ? src[i] : 0u;
-      const uint32_t d = (e >> sh) & 255u;
-      uint64_t peers = __ballot(valid);
+    for (uint32_t base0 = b0; base0 < b1; base0 += 64 * kSortBatch) {
+      uint32_t v[kSortBatch];
 #pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const uint64_t m = __ballot((d >> b) & 1);
-        peers &= ((d >> b) & 1) ? m : ~m;
+      for (uint32_t u = 0; u < kSortBatch; u++) {
+        const uint32_t i = base0 + 64 * u + lane;
+        v[u] = i < b1 ? src[i] : 0u;
       }
-      if (valid) {
-        const uint32_t rk = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-        const uint32_t off = hist[wave][d];
-        dst[off + rk] = e;
-        if (rk == 0) hist[wave][d] = off + (uint32_t)__popcll(peers);
+#pragma unroll
+      for (uint32_t u = 0; u < kSortBatch; u++) {
+        const uint32_t base = base0 + 64 * u;
+        if (base >= b1) break;
+        const uint32_t i = base + lane;
+        const bool valid = i < b1;
+        const uint32_t e = v[u];
+        const uint32_t d = (e >> sh) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          const uint64_t m = __ballot((d >> b) & 1);
+          peers &= ((d >> b) & 1) ? m : ~m;
+        }
+        if (valid) {
+          const uint32_t rk = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+          const uint32_t off = hist[wave][d];
+          dst[off + rk] = e;
+          if (rk == 0) hist[wave][d] = off + (uint32_t)__popcll(peers);
+        }
       }
     }
     __syncthreads();
@@ -437,11 +472,16 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
   uint32_t* pos32 = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   uint32_t* gs32 = pos32 + E;
   uint32_t carry = 0;
+  // the next tile's element and its predecessor are loaded one tile ahead
+  uint32_t eN = tid < E ? src[tid] : 0u, pN = tid > 0 && tid < E ? src[tid - 1] : 0u;
   for (uint32_t base = 0; base < E; base += kSortThreads) {
     const uint32_t s = base + tid;
     const bool valid = s < E;
-    const uint32_t e = valid ? src[s] : 0u;
-    const bool start = valid && (s == 0 || (e >> pb) != (src[s - 1] >> pb));
+    const uint32_t e = eN, ep = pN;
+    const uint32_t sn = s + kSortThreads;
+    eN = sn < E ? src[sn] : 0u;
+    pN = sn < E ? src[sn - 1] : 0u;
+    const bool start = valid && (s == 0 || (e >> pb) != (ep >> pb));
     uint32_t v = wave_incl_scan_max(start ? s + 1 : 0u);
     if (lane == 63) s_scan[wave] = v;
     __syncthreads();
@@ -498,6 +538,17 @@ struct Bytes<false> {
   __device__ __forceinline__ uint32_t ld4(uint64_t pos) const { return gload4(in, pos); }
 };
 
+// the segment's targets and window staged in LDS, the rest of the block (long extensions) from HBM
+struct BytesHybrid {
+  const uint32_t* w;
+  uint64_t base, lim;  // LDS holds [base, lim)
+  const uint8_t* in;
+  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const
+  {
+    return pos + 8 <= lim ? lload4(w, (uint32_t)(pos - base)) : gload4(in, pos);
+  }
+};
+
 // exact common prefix of p and c (capped at room) if it reaches `need`, else 0
 template <class Src>
 __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t p, uint64_t c, uint32_t need, uint32_t room)
@@ -543,6 +594,8 @@ constexpr uint32_t kSatQ = 128;  // saturated-candidate queue per wavefront (flu
 template <bool kLds>
 constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
+constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_long9
+constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
 
 // per-slot arrays written by k_sort: u16 when the segment's window fits 16 bits (same predicate there)
 __device__ __forceinline__ bool compact_small(const Segment& S) { return S.s1 - S.w0 <= 65536u; }
@@ -556,14 +609,16 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 }
 
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96))) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                               const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                               const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                               uint32_t maxChain, uint32_t* __restrict__ mlen,
-                                                              uint16_t* __restrict__ mdist, uint64_t matchBase)
+                                                              uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                                              uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
+  __shared__ uint32_t s_long;
   // -9: per wavefront, candidates whose first 12 bytes match (lane << 17 | slot) and the best
   // exact key of each lane among them
   __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
@@ -596,7 +651,10 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
   const uint64_t t0 = __builtin_readcyclecounter();
   uint64_t dB = 0, dL = 0, dBi = 0, dLi = 0;
 #endif
-  if (tid == 0) s_next = 0;
+  if (tid == 0) {
+    s_next = 0;
+    s_long = 0;
+  }
   Bytes<kLds> src;
   if constexpr (kLds) {
     const uint32_t words = (uint32_t)((B.end - S.w0 + 8 + 3) / 4);
@@ -648,7 +706,10 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
       limit = room < cap ? room : cap;
     }
     uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
-    bool isLong = false, run = active && bestLen < room && gs < slot;
+    // -9, a target with more than kBigGroup candidates (runs, periodic data): left to k_find_long9,
+    // which walks in text order and prunes with the previous target's result
+    const bool big = unlimited && cut == kNone && active && slot - gs > kBigGroup;
+    bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
     // the candidate at cpos passed the mask test: its exact prefix (extended past 12 from the text)
@@ -699,6 +760,7 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
       // extended from the text in batches of 64 (one per lane).
       uint32_t bestKey = 0;
       uint32_t qn = 0;
+      bool walk = false;  // phase 1: this lane still takes candidates inside the chunk
       satBest[lane] = 0;
       const uint32_t cap12 = limit < 12u ? limit : 12u;
       auto flush = [&]() {
@@ -726,6 +788,8 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
         }
         }
         qn = 0;
+        // candidates arrive nearest first: a lane whose match reached its cap is finished
+        if (satBest[lane] >= (limit << 17)) walk = run = false;
       };
       // lanes whose match can still grow past 12 bytes
       const uint64_t satOk = __ballot(limit > 12u);
@@ -752,7 +816,7 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
         const int32_t lo1 = (int32_t)(gs > first ? gs : first);
         uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
         int32_t cl = (int32_t)slot;
-        bool walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
+        walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
         while (__ballot(walk)) {
 #if SZ4_DIAG == 3
           dL++;
@@ -763,8 +827,9 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
           r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
           cl--;
           if (needWin && walk && rRel < lbRel) walk = run = false;
-          visit(walk, (uint32_t)cl, r0, r1, r2);
+          const bool mine = walk;
           walk = walk && cl > lo1;
+          visit(mine, (uint32_t)cl, r0, r1, r2);
         }
         run = run && (int32_t)gs < (int32_t)first;
       }
@@ -787,7 +852,8 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
               visit(run, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             }
           } else {
-            // no window test: every lane may take the candidate (only the group's lanes can match)
+            // no window test: every lane may take the candidate (only the group's lanes can match; a
+            // lane finished at its cap cannot move: its queued candidates never beat the one it has)
             for (int32_t k = 0; k < n; k++) {
 #if SZ4_DIAG == 3
               dB++;
@@ -795,6 +861,8 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
               visit(true, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             }
           }
+          // settle queued candidates every 256: a lane whose match reached its cap stops there
+          if (qn && ((uint32_t)(first - 1 - cBase) & 0xC0u) == 0xC0u) flush();
           cBase -= 64;
         }
       }
@@ -885,9 +953,13 @@ __global__ __launch_bounds__(kFindThreads, 2) void k_find_sorted(const uint8_t* 
     if (active) {
       const uint64_t idx = p - matchBase;
       mlen[idx] = isLong ? kLongMatch : (bestDist ? bestLen : 0u);
-      mdist[idx] = (uint16_t)bestDist;
+      mdist[idx] = (uint16_t)(big ? 0u : bestDist);  // pass 2's seed: the nearest candidate at the cap
+      if (isLong && unlimited) atomicOr(&longBits[idx >> 5], 1u << (idx & 31));
     }
+    if (unlimited && __ballot(active && isLong) && lane == 0) s_long = 1;
   }
+  __syncthreads();
+  if (tid == 0) segLong[blockIdx.x] = s_long;
 #if SZ4_DIAG == 3
   const uint64_t t2 = __builtin_readcyclecounter();
   const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
@@ -904,7 +976,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
                                                        const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                        const uint32_t* __restrict__ rankAll, uint32_t maxChain,
                                                        uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                       uint64_t matchBase)
+                                                       uint64_t matchBase, uint32_t* __restrict__ longFlag)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
@@ -1026,6 +1098,29 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
                 bestDist = carryDist;
               }
             }
+            // pass 1 left the nearest candidate that reached its cap: its exact prefix, 64 bytes
+            // per step over the row's 16 lanes, is a lower bound that ends most walks at once
+            if (curP1Dist != 0u && (curP1Dist < bestDist || bestDist == 0u || bestLen < room)) {
+              const uint64_t c = p - curP1Dist;
+              uint32_t k = 0, lcp = 0;
+              while (true) {
+                const uint32_t off = k + 4u * li;
+                const uint32_t x = off < room ? (src.ld4(p + off) ^ src.ld4(c + off)) : 0xFFFFFFFFu;
+                const uint32_t mis = (uint32_t)(__ballot(x != 0u) >> rowBase) & 0xFFFFu;
+                if (mis) {
+                  const uint32_t f = (uint32_t)__builtin_ctz(mis);
+                  const uint32_t xf = (uint32_t)__shfl(x, (int)(rowBase + f), 64);
+                  lcp = k + 4u * f + ((uint32_t)__builtin_ctz(xf) >> 3);
+                  break;
+                }
+                k += 64;
+              }
+              lcp = lcp < room ? lcp : room;
+              if (lcp > bestLen || (lcp == bestLen && curP1Dist < bestDist)) {
+                bestLen = lcp;
+                bestDist = curP1Dist;
+              }
+            }
           } else {
             bestLen = 1;
             bestDist = 0;
@@ -1122,6 +1217,296 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
       mlen[myIdx] = resLen;
       mdist[myIdx] = (uint16_t)resDist;
     }
+    // the parse keeps range minima for blocks with matches of kRmqLen+ (other than same-letter runs)
+    const bool rmqLen = lane < cnt && pass1Len == kLongMatch && resLen >= kRmqLen && !(resDist == 1u && resLen >= kSameLetter);
+    if (__ballot(rmqLen) && lane == 0) atomicOr(&longFlag[S.block], 1u);
+  }
+}
+
+// ================================================================================================
+// k_find_long9 (pass 2 at -9): the targets pass 1 left marked -- matches of kLongCap9+ bytes and
+// targets of groups larger than kBigGroup -- walked in text order.  A wavefront takes a chunk of 64
+// targets; every "stretch" of consecutive marked targets is walked by one wavefront from its head,
+// 64 candidates (nearest first) per step.  Two facts bound the walk:
+//   carry   if target p-1 has best match (d, L), candidate p - d has exactly L - 1 in common with p;
+//   pruning any candidate c' whose preceding byte equals data[p-1] (c' - 1 then being a candidate of
+//           p-1 with one more byte in common) has at most L - 1 in common with p, and if exactly
+//           L - 1 it is not nearer than d: it cannot win (the longest-previous-factor argument).
+//           Inside runs and periodic data such candidates form contiguous runs of sorted slots, and
+//           skip[s] (the slot below the run of s) jumps over them in one step.
+// Pruning needs p-1's result to be the reference's exact maximum (pass 1 / this pass), the carry to
+// be a valid candidate of p, and no lookback cut (stream blocks keep the plain walk).
+// ================================================================================================
+constexpr uint32_t kPiece = 1024;  // stretch pieces walked one after the other by one wavefront
+
+template <class Src>
+__device__ __forceinline__ uint32_t wave_exact_prefix(const Src& src, uint64_t p, uint64_t c, uint32_t room)
+{
+  const uint32_t lane = lane_id();
+  uint32_t k = 0;
+  while (true) {
+    const uint32_t off = k + 4u * lane;
+    const uint32_t x = off < room ? (src.ld4(p + off) ^ src.ld4(c + off)) : 0xFFFFFFFFu;
+    const uint64_t mis = __ballot(x != 0u);
+    if (mis) {
+      const uint32_t f = (uint32_t)__builtin_ctzll(mis);
+      const uint32_t xf = rdlane(x, f);
+      const uint32_t l = k + 4u * f + ((uint32_t)__builtin_ctz(xf) >> 3);
+      return l < room ? l : room;
+    }
+    k += 256;
+  }
+}
+
+template <bool kLds>
+__global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                             const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                             const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
+                                                             uint2* __restrict__ skipAll, const uint32_t* __restrict__ rankAll,
+                                                             const uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
+                                                             uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                             uint64_t matchBase, uint32_t* __restrict__ longFlag)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t win[];
+  __shared__ uint32_t s_next;
+  __shared__ uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
+  __shared__ uint32_t nEx;
+  __shared__ uint32_t s_scan[kFindThreads / 64];
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const void* compact = compactAll + S.elemOff;
+  const uint32_t* rank = rankAll + S.rankOff;
+  int32_t* skip = reinterpret_cast<int32_t*>(skipAll + S.elemOff);
+  const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
+  const uint32_t niv = ivCount[S.block];
+
+  // positions not inserted into the chains: shortcut intervals of this block and the previous one
+  if (tid == 0) {
+    uint32_t k = 0;
+    const uint32_t ids[2] = {B.prev, S.block};
+    for (int t = 0; t < 2; t++) {
+      if (ids[t] == kNoBlock) continue;
+      const Interval* ivb = ivAll + (uint64_t)ids[t] * kMaxIv;
+      for (uint32_t j = 0; j < ivCount[ids[t]]; j++) {
+        const uint64_t lo = ivb[j].lo > S.w0 ? ivb[j].lo : S.w0, hi = ivb[j].hi < S.s1 ? ivb[j].hi : S.s1;
+        if (lo < hi) {
+          exLo[k] = lo;
+          exHi[k] = hi;
+          k++;
+        }
+      }
+    }
+    nEx = k;
+    s_next = 0;
+  }
+  // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM
+  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
+  {
+    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
+    const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
+    src.w = win;
+    src.base = S.w0;
+    if constexpr (!kLds) {
+      src.lim = S.w0 + 4ull * words;
+      src.in = in;
+    }
+  }
+  __syncthreads();
+  const uint32_t ne = nEx;
+  uint32_t E = (uint32_t)(S.s1 - S.w0);
+  for (uint32_t j = 0; j < ne; j++) E -= (uint32_t)(exHi[j] - exLo[j]);
+  const bool small = compact_small(S);
+  auto excluded = [&](uint64_t q) -> bool {
+    for (uint32_t j = 0; j < ne; j++)
+      if (q >= exLo[j] && q < exHi[j]) return true;
+    return false;
+  };
+  // preceding byte of candidate position q, or 256 when q - 1 is not a chain position
+  auto pred_class = [&](uint64_t q) -> uint32_t {
+    if (q <= S.w0 || excluded(q - 1)) return 256u;
+    return src.ld4(q - 1) & 0xFFu;
+  };
+  auto long_bit = [&](uint64_t q) -> bool {
+    const uint64_t idx = q - matchBase;
+    return (longBits[idx >> 5] >> (idx & 31)) & 1u;
+  };
+
+  uint64_t cut = B.cut;
+  uint32_t cutHash = 0;
+  if (cut != kNone) {
+    const Interval* pv = ivAll + (uint64_t)B.prev * kMaxIv;
+    if (in_iv(pv, ivCount[B.prev], cut)) cut = kNone;
+    else cutHash = ref_hash(gload4(in, cut));
+  }
+  const uint64_t stopAbs = B.end - kTailLiterals;
+  const bool searched = segLong[blockIdx.x] != 0u;
+
+  // 1. skip[s] = the slot just below the run of equal preceding bytes that holds s (runs end at
+  //    group starts): an inclusive max-scan of run starts, tiles of 1024 slots
+  if (searched) {
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < E; base += kFindThreads) {
+      const uint32_t sl = base + tid;
+      const bool valid = sl < E;
+      bool start = true;
+      if (valid) {
+        const uint32_t g = slot_gs(compact, small, E, sl);
+        if (sl > g)
+          start = pred_class(S.w0 + slot_pos(compact, small, sl)) != pred_class(S.w0 + slot_pos(compact, small, sl - 1));
+      }
+      uint32_t v = wave_incl_scan_max(valid && start ? sl + 1 : 0u);
+      if (lane == 63) s_scan[wave] = v;
+      __syncthreads();
+      uint32_t pre = carry;
+      for (uint32_t w = 0; w < wave; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
+      v = v > pre ? v : pre;
+      if (valid) skip[sl] = (int32_t)v - 2;  // (run start) - 1
+      for (uint32_t w = wave; w < kFindThreads / 64; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
+      carry = pre;
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+
+  // best match of target p (wave-uniform): carry (cLen, cDist), exact = the carry is p-1's maximum
+  auto best_of = [&](uint64_t p, uint32_t cLen, uint32_t cDist, bool exact, uint32_t& bLen, uint32_t& bDist) {
+    const uint32_t key = src.ld4(p);
+    const uint32_t room = (uint32_t)(stopAbs - p);
+    uint64_t lb = p > kWindow ? p - kWindow : 0;
+    if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
+    uint32_t bestLen = 0, bestDist = 0;
+    bool carryOk = false;
+    if (cDist != 0u && cLen >= 5u) {
+      const uint64_t c = p - cDist;
+      if (c >= lb && !excluded(c)) {
+        bestLen = cLen - 1;
+        bestDist = cDist;
+        carryOk = true;
+      }
+    }
+    if (carryOk && bestLen >= room && bestDist == 1u) {
+      bLen = bestLen;  // as long as possible, and no candidate is nearer
+      bDist = 1;
+      return;
+    }
+    const uint32_t slot = rank[p - S.s0];
+    const int32_t gs = (int32_t)slot_gs(compact, small, E, slot);
+    const bool prune = exact && cut == kNone && (carryOk || cLen < 5u);
+    const uint32_t pc = prune ? (src.ld4(p - 1) & 0xFFu) : 0xFFFFu;
+    // pass 1's nearest candidate at its cap
+    const uint32_t seed = mdist[p - matchBase];
+    if (seed != 0u && (bestLen < room || seed < bestDist)) {
+      const uint32_t l = wave_exact_prefix(src, p, p - seed, room);
+      if (l > bestLen || (l == bestLen && seed < bestDist)) {
+        bestLen = l;
+        bestDist = seed;
+      }
+    }
+    int32_t s = (int32_t)slot - 1;
+    if (bestDist == 0u && s >= gs) {
+      // nothing known yet: the nearest candidate's exact prefix, 256 bytes per step, so that the walk
+      // below rejects the others at a glance
+      const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)s);
+      if (c >= lb && src.ld4(c) == key) {
+        bestLen = wave_exact_prefix(src, p, c, room);
+        bestDist = (uint32_t)(p - c);
+        s--;
+      }
+    }
+    while (s >= gs) {
+      const int32_t sl = s - (int32_t)lane;
+      const bool inG = sl >= gs;
+      const uint64_t c = inG ? S.w0 + slot_pos(compact, small, (uint32_t)sl) : 0u;
+      const bool below = inG && c < lb;  // positions descend: everything farther is out of the window
+      const bool valid = inG && !below;
+      const bool pruned = valid && prune && pred_class(c) == pc;
+      const uint64_t inMask = __ballot(inG);
+      if (!__ballot(below) && __ballot(pruned) == inMask && inMask == ~0ull) {
+        s = skip[s - 63];  // the whole step is one run of pruned candidates: below that run
+        continue;
+      }
+      const uint32_t dist = (uint32_t)(p - c);
+      uint32_t got = 0;
+      if (valid && !pruned && src.ld4(c) == key) {
+        const uint32_t need = bestDist == 0u ? 4u : (dist < bestDist ? bestLen : bestLen + 1u);
+        got = prefix_if_at_least(src, p, c, need < 4u ? 4u : need, room);
+        if (got < need) got = 0;
+      }
+      // longest, then nearest (lower lane)
+      uint64_t top = wave_max_u64(got ? ((uint64_t)got << 6) | (63u - lane) : 0ull);
+      if (top) {
+        const uint32_t tl = (uint32_t)(top >> 6), wl = 63u - (uint32_t)(top & 63u);
+        const uint32_t wd = rdlane(dist, wl);
+        if (tl > bestLen || (tl == bestLen && wd < bestDist)) {
+          bestLen = tl;
+          bestDist = wd;
+        }
+      }
+      if (__ballot(below)) break;
+      const uint32_t lastLane = (uint32_t)(63 - __builtin_clzll(inMask));
+      const uint32_t farDist = rdlane(dist, lastLane);
+      if (bestDist != 0u && bestLen >= room && farDist >= bestDist) break;  // only nearer ties could win
+      s -= 64;
+    }
+    if (bestDist == 0u) bestLen = 0;
+    bLen = bestLen;
+    bDist = bestDist;
+  };
+
+  const uint32_t nTargets = (uint32_t)(S.s1 - S.s0);
+  while (true) {
+    uint32_t chunkIdx = 0;
+    if (lane == 0) chunkIdx = atomicAdd(&s_next, 1u);
+    chunkIdx = rdlane(chunkIdx, 0);
+    const uint32_t first = chunkIdx * 64;
+    if (first >= nTargets) break;
+    const uint32_t cnt = nTargets - first < 64 ? nTargets - first : 64;
+    const uint64_t p = S.s0 + first + lane;
+    const uint64_t myIdx = p - matchBase;
+    const uint32_t p1 = lane < cnt ? mlen[myIdx] : 0u;
+    if (__ballot(p1 == kLongMatch) == 0) continue;
+    const bool lg = lane < cnt && long_bit(p);
+    // marked but never sorted: shortcut-interval targets copy the predecessor's match, minus one
+    if (lane < cnt && p1 == kLongMatch && !lg) {
+      for (uint32_t k = 0; k < niv; k++)
+        if (p >= iv[k].lo && p < iv[k].hi) {
+          mlen[myIdx] = (uint32_t)(iv[k].La - (p - iv[k].a));
+          mdist[myIdx] = 1;
+        }
+    }
+    // stretch heads: marked targets whose predecessor is not (or lies before the segment); long
+    // stretches are cut every kPiece targets so that they run in parallel
+    const bool head = lg && (p == S.s0 || ((p - S.s0) & (kPiece - 1)) == 0 || !long_bit(p - 1));
+    uint64_t heads = __ballot(head);
+    while (heads) {
+      const uint32_t h = (uint32_t)__builtin_ctzll(heads);
+      heads &= heads - 1;
+      uint64_t q = S.s0 + first + h;
+      // p-1's result: final when it is a target of this block that pass 1 finished
+      uint32_t cLen = 0, cDist = 0;
+      bool exact = false;
+      if (q > B.start && !long_bit(q - 1) && !(niv && in_iv(iv, niv, q - 1))) {
+        cLen = mlen[q - 1 - matchBase];
+        cDist = mdist[q - 1 - matchBase];
+        exact = true;
+      }
+      while (true) {
+        uint32_t bLen, bDist;
+        best_of(q, cLen, cDist, exact, bLen, bDist);
+        if (lane == 0) {
+          mlen[q - matchBase] = bLen;
+          mdist[q - matchBase] = (uint16_t)bDist;
+          if (bLen >= kRmqLen && !(bDist == 1u && bLen >= kSameLetter)) atomicOr(&longFlag[S.block], 1u);
+        }
+        cLen = bLen;
+        cDist = bDist;
+        exact = true;
+        q++;
+        if (q >= S.s1 || ((q - S.s0) & (kPiece - 1)) == 0 || !long_bit(q)) break;
+      }
+    }
   }
 }
 
@@ -1148,6 +1533,298 @@ __device__ __forceinline__ uint32_t len_extra(uint32_t len)
 {
   return len < 19 ? 3u : 4u + (len - 19) / 255;
 }
+
+// ------------------------------------------------------------------------------------------------
+// Long lengths of the optimal parse.  A position with match length Lk > 64 takes
+//   min over l in (64, Lk] of cost[i + l] + extra(l),  ties to the longest,
+// with extra(l) = 4 + (l - 19) / 255, constant on pieces l in [19 + 255k, 273 + 255k].  The reference
+// scans every l (smallz4.h:421-448); here:
+//   A  l in [65, 273]: one wavefront step, four consecutive lengths per lane;
+//   B  pieces k >= 1: a piece is a window of 255 positions, so it spans at most two 256-position
+//      "rmq blocks" (aligned on the block's last parsed position `top`), and its minimum is
+//      min(UP[a], DOWN[b]): UP[j] = min key over [j, top of j's rmq block], DOWN[j] = min key over
+//      [bottom of j's rmq block, j], key = cost << 8 | (top - j) & 255 (ties: highest position).
+//      One lane per piece;
+//   C  a last partial piece inside one rmq block and aligned to neither end: scanned directly.
+// Positions above `above` cost 0 (the guess above a speculative segment; the block tail).
+// UP/DOWN exist only for blocks whose matches reach 274 bytes (longFlag, set by k_find); without
+// them the pieces are scanned (never taken when the flag is right).
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rmq_key(uint32_t cost, int32_t top, int32_t j)
+{
+  return (cost << 8) | ((uint32_t)(top - j) & 255u);
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan_min(uint32_t v)
+{
+  const uint32_t lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d && o < v) v = o;
+  }
+  return v;
+}
+
+// UP of the chunk [hi - cnt + 1, hi] (lane t = position hi - t, key kt).  The chunk lies inside one
+// rmq block; upCarry = UP[hi + 1] when hi + 1 is in the same block.
+__device__ __forceinline__ void rmq_store_up(uint32_t* up, int32_t top, int32_t hi, uint32_t cnt, uint32_t kt,
+                                             uint32_t& upCarry)
+{
+  const uint32_t lane = lane_id();
+  const bool blockTop = ((uint32_t)(top - hi) & 255u) == 0u;
+  uint32_t v = wave_incl_scan_min(lane < cnt ? kt : 0xFFFFFFFFu);
+  if (!blockTop) v = min(v, upCarry);
+  if (lane < cnt) up[hi - (int32_t)lane] = v;
+  upCarry = rdlane(v, 63);
+}
+
+// top of the rmq block holding position j
+__device__ __forceinline__ int32_t rmq_block_top(int32_t top, int32_t j)
+{
+  return top - (int32_t)(((uint32_t)(top - j) >> 8) << 8);
+}
+
+// DOWN of the rmq block [jb, its top] (every position final); cost_of(j) is the exact cost
+template <class CostOf>
+__device__ __forceinline__ void rmq_store_down(uint32_t* down, int32_t top, int32_t jb, CostOf cost_of)
+{
+  const uint32_t lane = lane_id();
+  const int32_t jt = rmq_block_top(top, jb);
+  uint32_t carry = 0xFFFFFFFFu;
+  for (int32_t j0 = jb; j0 <= jt; j0 += 64) {
+    const int32_t j = j0 + (int32_t)lane;
+    uint32_t v = j <= jt ? rmq_key(cost_of(j), top, j) : 0xFFFFFFFFu;
+    v = min(wave_incl_scan_min(v), carry);
+    if (j <= jt) down[j] = v;
+    carry = rdlane(v, 63);
+  }
+}
+
+// UP of a whole rmq block [jb, jt]
+template <class CostOf>
+__device__ __forceinline__ void rmq_store_up_block(uint32_t* up, int32_t top, int32_t jb, int32_t jt, CostOf cost_of)
+{
+  const uint32_t lane = lane_id();
+  uint32_t carry = 0xFFFFFFFFu;
+  for (int32_t j0 = jt; j0 >= jb; j0 -= 64) {
+    const int32_t j = j0 - (int32_t)lane;
+    uint32_t v = j >= jb ? rmq_key(cost_of(j), top, j) : 0xFFFFFFFFu;
+    v = min(wave_incl_scan_min(v), carry);
+    if (j >= jb) up[j] = v;
+    carry = rdlane(v, 63);
+  }
+}
+
+// minimum of cost_at(i + l) + extra over l in [l0, l1] (l1 - l0 < 256), four lengths per lane,
+// folded into (minCost, best) with ties to the longest
+template <class CostAt>
+__device__ __forceinline__ void scan_lengths(int32_t i, uint32_t l0, uint32_t l1, uint32_t extra, int32_t above,
+                                             CostAt cost_at, uint32_t& minCost, uint32_t& best)
+{
+  const uint32_t lane = lane_id();
+  uint32_t c = 0xFFFFFFFFu, lb = 0;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; u++) {
+    const uint32_t l = l0 + 4u * lane + u;
+    if (l <= l1) {
+      const int32_t j = i + (int32_t)l;
+      const uint32_t cj = j > above ? 0u : cost_at(j);
+      if (cj <= c) {
+        c = cj;
+        lb = l;
+      }
+    }
+  }
+  const uint32_t key = c == 0xFFFFFFFFu ? 0xFFFFFFFFu : ((c + extra) << 8) | (255u - lane);
+  const uint32_t km = wave_min_fast(key);
+  if (km != 0xFFFFFFFFu && (km >> 8) <= minCost) {
+    minCost = km >> 8;
+    best = rdlane(lb, 255u - (km & 255u));
+  }
+}
+
+// cost_at(j): exact cost of a position j in (i, above]; key_cost(j, key): exact cost encoded by an
+// UP/DOWN key stored at position j.  Folds lengths 65 .. Lk into (minCost, best).
+template <class CostAt, class KeyCost>
+__device__ __forceinline__ void long_lengths(int32_t i, uint32_t Lk, int32_t top, int32_t above, bool rmq,
+                                             const uint32_t* up, const uint32_t* down, CostAt cost_at,
+                                             KeyCost key_cost, uint32_t& minCost, uint32_t& best)
+{
+  const uint32_t lane = lane_id();
+  // A: lengths 65 .. 273 (piece 0)
+  scan_lengths(i, 65u, Lk < 273u ? Lk : 273u, 4u, above, cost_at, minCost, best);
+  if (Lk < kRmqLen) return;
+  const uint32_t K = (Lk - 19u) / 255u;  // pieces 1 .. K
+  if (!rmq) {
+    for (uint32_t k = 1; k <= K; k++) {
+      const uint32_t l0 = 19u + 255u * k, l1 = 273u + 255u * k < Lk ? 273u + 255u * k : Lk;
+      scan_lengths(i, l0, l1, 4u + k, above, cost_at, minCost, best);
+    }
+    return;
+  }
+  // B: lane t takes piece kb + t
+  bool direct = false;  // the last piece needs part C
+  for (uint32_t kb = 1; kb <= K; kb += 64) {
+    const uint32_t k = kb + lane;
+    uint32_t key = 0xFFFFFFFFu, lsel = 0;
+    if (k <= K) {
+      const uint32_t la = 19u + 255u * k, lbnd = 273u + 255u * k < Lk ? 273u + 255u * k : Lk;
+      const int32_t a = i + (int32_t)la, b = i + (int32_t)lbnd;
+      uint32_t c = 0xFFFFFFFFu;
+      if (b > above) {
+        c = 0;  // zero costs above: the longest length of the piece
+        lsel = lbnd;
+      } else {
+        const uint32_t ra = (uint32_t)(top - a), rb = (uint32_t)(top - b);
+        const bool sameBlock = (ra >> 8) == (rb >> 8);
+        const bool useUp = !sameBlock || (rb & 255u) == 0u;      // [a, top of a's block] inside the piece
+        const bool useDown = !sameBlock || (ra & 255u) == 255u;  // [bottom of b's block, b] inside it
+        if (!useUp && !useDown) {
+          direct = true;  // only the last piece can be this short
+        } else {
+          uint32_t cu = 0xFFFFFFFFu, cd = 0xFFFFFFFFu;
+          int32_t ju = 0, jd = 0;
+          if (useUp) {
+            const uint32_t kU = ld_fresh(&up[a]);
+            ju = top - (int32_t)(((ra >> 8) << 8) + (kU & 255u));
+            cu = key_cost(a, kU);
+          }
+          if (useDown) {
+            const uint32_t kD = ld_fresh(&down[b]);
+            jd = top - (int32_t)(((rb >> 8) << 8) + (kD & 255u));
+            cd = key_cost(b, kD);
+          }
+          // the DOWN side holds the higher positions: it wins ties
+          if (cd <= cu) {
+            c = cd;
+            lsel = (uint32_t)(jd - i);
+          } else {
+            c = cu;
+            lsel = (uint32_t)(ju - i);
+          }
+        }
+      }
+      if (c != 0xFFFFFFFFu) key = ((c + 4u + k) << 8) | (255u - lane);
+    }
+    const uint32_t km = wave_min_fast(key);
+    if (km != 0xFFFFFFFFu && (km >> 8) <= minCost) {
+      minCost = km >> 8;
+      best = rdlane(lsel, 255u - (km & 255u));
+    }
+  }
+  // C: the last piece, scanned
+  if (__ballot(direct)) scan_lengths(i, 19u + 255u * K, Lk, 4u + K, above, cost_at, minCost, best);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Long carried matches.  Along a repeat, consecutive positions share the end E = i + Lk of their
+// match (a run of zeros: every position).  Since extra(a) + extra(b) >= extra(a + b) + 2 for any
+// a >= 4, b >= 1 (extra(x) = 3 for x < 19), if every j in (i, E) has
+//     cost[j] - extra(E - j) >= cost[E] - 2                                   (margin test)
+// then every length l < Lk costs cost[i+l] + extra(l) >= cost[E] + extra(E - i): the full length is
+// optimal among the matches (and wins ties, being the longest).  With costs flat above a speculative
+// segment (the guess 0), E is the first position above it and the best length is the longest one of
+// extra(E - i).  The running minimum `margin` of cost[j] - extra(E - j) is kept per position; it is
+// established once per chain with range minima (end_margin), so a chain costs O(1) per position.
+// ------------------------------------------------------------------------------------------------
+constexpr int32_t kMarginBias = 1 << 30;
+
+// minimum cost over [a, b] (b - a < 255) from UP/DOWN, or 0xFFFFFFFF when the range lies inside one
+// rmq block aligned to neither end (the caller scans it)
+template <class KeyCost>
+__device__ __forceinline__ uint32_t rmq_range_cost(int32_t a, int32_t b, int32_t top, const uint32_t* up,
+                                                   const uint32_t* down, KeyCost key_cost)
+{
+  const uint32_t ra = (uint32_t)(top - a), rb = (uint32_t)(top - b);
+  const bool sameBlock = (ra >> 8) == (rb >> 8);
+  const bool useUp = !sameBlock || (rb & 255u) == 0u;
+  const bool useDown = !sameBlock || (ra & 255u) == 255u;
+  if (!useUp && !useDown) return 0xFFFFFFFFu;
+  uint32_t c = 0xFFFFFFFFu;
+  if (useUp) c = key_cost(a, ld_fresh(&up[a]));
+  if (useDown) {
+    const uint32_t cd = key_cost(b, ld_fresh(&down[b]));
+    c = cd < c ? cd : c;
+  }
+  return c;
+}
+
+// min over j in [i + 1, E - 1] of cost[j] - extra(E - j), + kMarginBias (wave-uniform)
+template <class CostAt, class KeyCost>
+__device__ __forceinline__ uint32_t end_margin(int32_t i, int32_t E, int32_t top, const uint32_t* up,
+                                               const uint32_t* down, CostAt cost_at, KeyCost key_cost)
+{
+  const uint32_t lane = lane_id();
+  uint32_t m = 0xFFFFFFFFu;
+  // distances 1 .. 273 from E (pieces of extra 3 and 4): scanned, five per lane
+#pragma unroll
+  for (uint32_t u = 0; u < 5; u++) {
+    const uint32_t D = 1u + 5u * lane + u;
+    const int32_t j = E - (int32_t)D;
+    if (D <= 273u && j > i) {
+      const uint32_t v = cost_at(j) + kMarginBias - len_extra(D);
+      m = v < m ? v : m;
+    }
+  }
+  const uint32_t Dmax = (uint32_t)(E - i - 1);
+  if (Dmax >= kRmqLen) {
+    const uint32_t K = (Dmax - 19u) / 255u;  // pieces 1 .. K (the last one clipped at i + 1)
+    bool direct = false;
+    for (uint32_t kb = 1; kb <= K; kb += 64) {
+      const uint32_t k = kb + lane;
+      if (k <= K) {
+        const int32_t b = E - 19 - 255 * (int32_t)k;
+        const int32_t a0 = E - 273 - 255 * (int32_t)k;
+        const int32_t a = a0 > i + 1 ? a0 : i + 1;
+        const uint32_t c = rmq_range_cost(a, b, top, up, down, key_cost);
+        if (c == 0xFFFFFFFFu) {
+          direct = true;
+        } else {
+          const uint32_t v = c + kMarginBias - (4u + k);
+          m = v < m ? v : m;
+        }
+      }
+    }
+    if (__ballot(direct)) {
+      const int32_t b = E - 19 - 255 * (int32_t)K;
+      const int32_t a0 = E - 273 - 255 * (int32_t)K;
+      const int32_t a = a0 > i + 1 ? a0 : i + 1;
+#pragma unroll
+      for (int32_t u = 0; u < 4; u++) {
+        const int32_t j = a + 4 * (int32_t)lane + u;
+        if (j <= b) {
+          const uint32_t v = cost_at(j) + kMarginBias - (4u + K);
+          m = v < m ? v : m;
+        }
+      }
+    }
+  }
+  return wave_min_fast(m);
+}
+
+// longest length with extra(len) == extra(x)
+__device__ __forceinline__ uint32_t piece_end(uint32_t x)
+{
+  return x < 19u ? 18u : 273u + 255u * ((x - 19u) / 255u);
+}
+
+// chain state of the carried-match shortcut (wave-uniform)
+// A chain is established at the first long position whose end differs (pending) and becomes valid at
+// the chunk flush, once every position above the next one is stored with its UP/DOWN keys.
+struct RunEnd {
+  int32_t E = -1;
+  uint32_t costE = 0;
+  uint32_t margin = 0;  // + kMarginBias
+  bool valid = false;
+  bool pending = false;
+  __device__ __forceinline__ void add(int32_t j, uint32_t c)
+  {
+    if (!valid) return;
+    const uint32_t v = c + kMarginBias - len_extra((uint32_t)(E - j));
+    margin = v < margin ? v : margin;
+  }
+};
 
 __global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, const uint32_t* __restrict__ ivCount,
                                              uint32_t maxChain, uint32_t* __restrict__ mlen, uint64_t matchBase,
@@ -1208,12 +1885,15 @@ __global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, c
 
 constexpr int kSpecWaves = 4;  // independent segments per workgroup (workgroup slots, not LDS, bound occupancy)
 
+template <bool kRmq>
 __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __restrict__ blocks,
                                                              const DpSeg* __restrict__ dpSegs, uint32_t ndp,
                                                              const uint32_t* __restrict__ mlen,
                                                              const uint16_t* __restrict__ mdist, uint64_t matchBase,
                                                              uint32_t* __restrict__ costAll, uint32_t* __restrict__ sel,
-                                                             uint32_t* __restrict__ reach, uint4* __restrict__ segState)
+                                                             uint32_t* __restrict__ reach, uint4* __restrict__ segState,
+                                                             const uint32_t* __restrict__ longFlag,
+                                                             uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll)
 {
   __shared__ uint32_t rings[kSpecWaves][kRing];
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform
@@ -1229,6 +1909,15 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   uint32_t* cost = costAll + base;
   uint32_t* S = sel + base;
   const int32_t segLo = (int32_t)G.lo, segHi = (int32_t)G.hi;
+  // long lengths (> 273): UP/DOWN range minima over rmq blocks aligned on the block's last parsed position
+  const int32_t top = (int32_t)(B.end - B.start) - 1 - kTailLiterals;
+  // blocks with matches of kRmqLen+ run in the kRmq instantiation (range minima, carried chains);
+  // the others in the lean one
+  const bool rmq = longFlag[G.block] != 0u;
+  if (rmq != kRmq) return;
+  uint32_t* up = upAll + base;
+  uint32_t* down = downAll + base;
+  uint32_t upCarry = 0xFFFFFFFFu;
 
   // reach[i] = max over q in [lo, i) of q + len[q]: the highest cost a position below i reads
   if (G.k > 0) {
@@ -1262,12 +1951,8 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   uint32_t litBump = 15;  // literal-run length at which a literal costs one more byte (15, 270, ...)
   uint32_t costNext = 0;  // cost[i + 1]
   uint32_t nextL = segHi - (int32_t)lane >= segLo ? L[segHi - lane] : 0u;
-  // cost read-back above the register window
-  auto far_cost = [&](int32_t i, uint32_t ln) -> uint32_t {
-    const int32_t j = i + (int32_t)ln;
-    if (j > segHi) return 0u;
-    return ln < (uint32_t)kRing - 64u ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
-  };
+  auto key_cost = [&](int32_t, uint32_t key) -> uint32_t { return key >> 8; };
+  RunEnd chain;
 
   for (int32_t hi = segHi; hi >= segLo; hi -= 64) {
     const int32_t lo = hi - 63 > segLo ? hi - 63 : segLo;
@@ -1278,6 +1963,45 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
     nextL = iN >= segLo ? L[iN] : 0u;  // prefetch the next chunk
     // per position hi - t in lane t: its best key (0 = slow path, see bestBuf), its cost, its choice
     uint32_t kvBuf = 0xFFFFFFFFu, mcBuf = 0, bestBuf = 1;
+    const uint32_t cnt = (uint32_t)(hi - lo + 1);
+    if (__ballot(lane < cnt && myL >= (uint32_t)kMinMatch) == 0) {
+      // no match anywhere in the chunk: every position is a literal, costs in closed form
+      const uint32_t t = lane, run = lits + t + 1u;
+      const uint32_t nb = run >= litBump ? 1u + (run - litBump) / 255u : 0u;
+      mcBuf = costNext + t + 1u + nb;
+      const uint32_t nbLast = rdlane(nb, cnt - 1u);
+      costNext = rdlane(mcBuf, cnt - 1u);
+      lits += cnt;
+      litBump += 255u * nbLast;
+      // next window: lane l = cost[lo + l] (position lo + l is lane cnt - 1 - l; only a full chunk has a next)
+      win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((63u - lane) << 2), (int)mcBuf) << 6;
+      chain.valid = chain.pending = false;
+    } else if (kRmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
+               [&]() -> bool {
+                 // every position continues the chain (a same-letter run position only when its end
+                 // is the chain's end inside the segment: its length is not the flat optimum)
+                 const int32_t i = hi - (int32_t)lane;
+                 const bool in = lane < cnt;
+                 const uint32_t Dl = in && myL >= kSameLetter ? (uint32_t)D[i] : 0u;
+                 const int32_t Ei = i + (int32_t)myL > segHi ? segHi + 1 : i + (int32_t)myL;
+                 const bool ok = !in || (myL >= (uint32_t)kMinMatch &&
+                                         (Dl == 1u ? (i + (int32_t)myL == chain.E && chain.E <= segHi) : Ei == chain.E));
+                 return __ballot(!ok) == 0;
+               }() &&
+               chain.costE + len_extra((uint32_t)(chain.E - hi)) <= costNext + 1u + (lits + 1u == litBump ? 1u : 0u)) {
+      // chain chunk: every position takes its full length (the longest of its extra when flat above)
+      const int32_t i = hi - (int32_t)lane;
+      const uint32_t x = (uint32_t)(chain.E - i);
+      mcBuf = chain.costE + len_extra(x);
+      kvBuf = 0;
+      bestBuf = i + (int32_t)myL > chain.E ? min(myL, piece_end(x)) : myL;
+      costNext = rdlane(mcBuf, cnt - 1u);
+      lits = 0;
+      litBump = 15;
+      const uint32_t mE = chain.costE + kMarginBias;
+      chain.margin = mE < chain.margin ? mE : chain.margin;
+      win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((63u - lane) << 2), (int)mcBuf) << 6;
+    } else
     for (uint32_t t = 0; t < 64; t += 4) {
       const int32_t i0 = hi - (int32_t)t;
       if (i0 < lo) break;
@@ -1321,6 +2045,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
           mcBuf = wrlane(mcBuf, c, t + (uint32_t)r);
         }
         litBump = anyMatch ? 15u : litBump;
+        chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
       } else {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -1341,23 +2066,57 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
               const int32_t j = i + (int32_t)Lk;  // far back: spilled
               minCost = (j > segHi ? 0u : ld_fresh(&cost[j])) + 4 + (Lk - 19) / 255;
             } else {
-              const uint32_t kmin = kv[r];
-              if ((kmin >> 6) <= minCost) {
-                minCost = kmin >> 6;
-                best = 64u - (kmin & 63u);
-              }
-              // lengths beyond 64: LDS ring (flushed every 64 positions), then the HBM spill
-              for (uint32_t b = 65; b <= Lk; b += 64) {
-                const uint32_t ln = b + lane;
-                uint32_t k2 = 0xFFFFFFFFu;
-                if (ln <= Lk) k2 = ((far_cost(i, ln) + len_extra(ln)) << 6) | (63u - lane);
-                const uint32_t km = wave_min_fast(k2);
-                if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
-                  minCost = km >> 6;
-                  best = b + (63u - (km & 63u));
+              auto cost_at = [&](int32_t j) -> uint32_t {
+                return j - i < kRing - 64 ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
+              };
+              const int32_t Ei = i + (int32_t)Lk > segHi ? segHi + 1 : i + (int32_t)Lk;
+              if (kRmq && Lk >= kRmqLen && chain.valid && chain.E == Ei && chain.margin + 2u >= chain.costE + kMarginBias) {
+                // carried match, margin test passed: the full length (longest of its extra when flat above)
+                const uint32_t x = (uint32_t)(Ei - i);
+                const uint32_t l = i + (int32_t)Lk > Ei ? min(Lk, piece_end(x)) : Lk;
+                const uint32_t mc = chain.costE + len_extra(x);
+                if (mc <= minCost) {
+                  minCost = mc;
+                  best = l;
+                }
+              } else {
+                const uint32_t kmin = kv[r];
+                if ((kmin >> 6) <= minCost) {
+                  minCost = kmin >> 6;
+                  best = 64u - (kmin & 63u);
+                }
+                // lengths beyond 64: LDS ring (flushed every 64 positions), the HBM spill, UP/DOWN
+                if (Lk > 64u) {
+                  if constexpr (kRmq) {
+                    long_lengths(i, Lk, top, segHi, true, up, down, cost_at, key_cost, minCost, best);
+                  } else {
+                    // no length reaches kRmqLen here: at most four steps
+                    for (uint32_t b = 65; b <= Lk; b += 64) {
+                      const uint32_t ln = b + lane;
+                      uint32_t k2 = 0xFFFFFFFFu;
+                      if (ln <= Lk) k2 = ((i + (int32_t)ln > segHi ? 0u : cost_at(i + (int32_t)ln)) + len_extra(ln)) << 6 | (63u - lane);
+                      const uint32_t km = wave_min_fast(k2);
+                      if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
+                        minCost = km >> 6;
+                        best = b + (63u - (km & 63u));
+                      }
+                    }
+                  }
+                }
+                if (kRmq && Lk >= kRmqLen) {
+                  chain.E = Ei;
+                  chain.costE = Ei > segHi ? 0u : cost_at(Ei);
+                  // at the chunk top every position above is stored: the margin right away
+                  chain.valid = i == hi;
+                  chain.pending = i != hi;
+                  if (i == hi) chain.margin = end_margin(i, Ei, top, up, down, cost_at, key_cost);
                 }
               }
             }
+          }
+          if constexpr (kRmq) {
+            if (Lk >= (uint32_t)kMinMatch && (i + (int32_t)Lk > segHi ? segHi + 1 : i + (int32_t)Lk) == chain.E) chain.add(i, minCost);
+            else chain.valid = chain.pending = false;  // chains are contiguous
           }
           mcost[r] = minCost;
           costNext = minCost;
@@ -1383,6 +2142,20 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
       ring[iMine & (kRing - 1)] = mcBuf;
       cost[iMine] = mcBuf;  // read back (sc1) only >= kRing-64 positions later: no fence needed here
     }
+    if constexpr (kRmq) {
+      rmq_store_up(up, top, hi, cnt, rmq_key(mcBuf, top, iMine), upCarry);
+      if (lo == 0 || ((uint32_t)(top - lo) & 255u) == 255u)
+        rmq_store_down(down, top, lo, [&](int32_t j) -> uint32_t { return ring[j & (kRing - 1)]; });
+      if (chain.pending) {
+        const int32_t i = lo - 1;
+        auto cost_at = [&](int32_t j) -> uint32_t {
+          return j - i < kRing - 64 ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
+        };
+        chain.margin = end_margin(i, chain.E, top, up, down, cost_at, key_cost);
+        chain.valid = true;
+        chain.pending = false;
+      }
+    }
   }
   if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, 0u, 0u);
 }
@@ -1391,11 +2164,13 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                                                const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
                                                uint64_t matchBase, uint32_t* __restrict__ costAll,
                                                uint32_t* __restrict__ sel, const uint32_t* __restrict__ reach,
-                                               uint4* __restrict__ segState)
+                                               uint4* __restrict__ segState, const uint32_t* __restrict__ longFlag,
+                                               uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll)
 {
   __shared__ uint32_t ring[kRing];
   __shared__ uint32_t convTab[kMaxDpSegs];   // positions >= convTab[k] of segment k hold exact costs
   __shared__ uint32_t deltaTab[kMaxDpSegs];  // below it: exact = stored + deltaTab[k]
+  __shared__ uint32_t convBlk[kMaxDpSegs];   // UP/DOWN keys of positions below it: exact = key cost + deltaTab[k]
   const Block B = blocks[blockIdx.x];
   if (B.dpCount <= 1) return;
   const uint32_t lane = threadIdx.x;
@@ -1406,9 +2181,14 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   uint32_t* cost = costAll + base;
   uint32_t* S = sel + base;
   const uint32_t first = dpSegs[B.dpFirst].hi;  // n - 6: the last parsed position
+  const int32_t top = (int32_t)first;
+  const bool rmq = longFlag[blockIdx.x] != 0u;
+  uint32_t* up = upAll + base;
+  uint32_t* down = downAll + base;
   if (lane == 0) {
     convTab[0] = 0;  // the top segment was parsed exactly
     deltaTab[0] = 0;
+    convBlk[0] = 0;
   }
   __syncthreads();
   // exact cost of a position above the segment being repaired (0 past the parsed range)
@@ -1431,16 +2211,91 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       if (j > hi) return exact_above((uint32_t)j);
       return j - i < kRing ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]);
     };
+    // exact cost encoded by an UP/DOWN key at j: this pass's own inside the segment, the tables above
+    auto key_cost = [&](int32_t j, uint32_t key) -> uint32_t {
+      uint32_t c = key >> 8;
+      if (j > hi) {
+        const uint32_t kk = (first - (uint32_t)j) / B.dpSize;
+        if ((uint32_t)j < convBlk[kk]) c += deltaTab[kk];
+      }
+      return c;
+    };
     uint32_t prevDelta = 0;
     int32_t runTop = hi;
     int32_t conv = lo;
     uint32_t convDelta = 0;
+    uint32_t upCarry = 0xFFFFFFFFu;
+    RunEnd chain;
     bool done = false;
     for (int32_t h = hi; h >= lo && !done; h -= 64) {
       const int32_t ip = h - (int32_t)lane;
       const bool in = ip >= lo;
       const uint32_t cL = in ? L[ip] : 0u, cD = in ? (uint32_t)D[ip] : 0u;
       const uint32_t cS = in ? S[ip] : 0u, cC = in ? cost[ip] : 0u, cR = in ? R[ip] : 0u;
+      const int32_t cl = h - 63 > lo ? h - 63 : lo;
+      const uint32_t cnt = (uint32_t)(h - cl + 1);
+      if (__ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
+        // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
+        auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
+          const uint32_t run = lits + t + 1u;
+          nb = run >= litBump ? 1u + (run - litBump) / 255u : 0u;
+          return costNext + t + 1u + nb;
+        };
+        uint32_t nb = 0, nb2 = 0;
+        const uint32_t cT = lit_cost(lane, nb);
+        if (lane < cnt) {
+          S[ip] = 1;
+          cost[ip] = cT;
+          ring[ip & (kRing - 1)] = cT;
+        }
+        // register window: lane l holds the cost of the position congruent to l mod 64
+        const uint32_t tl = ((uint32_t)h - lane) & 63u;
+        if (tl < cnt) cbuf = lit_cost(tl, nb2);
+        chain.valid = chain.pending = false;
+        const uint32_t delta = cT - cC;
+        uint32_t dPrev = __shfl_up(delta, 1, 64);
+        if (lane == 0) dPrev = prevDelta;
+        const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
+        if (chg) runTop = h - (63 - (int32_t)__builtin_clzll(chg));
+        prevDelta = rdlane(delta, cnt - 1u);
+        lits += cnt;
+        litBump += 255u * rdlane(nb, cnt - 1u);
+        costNext = rdlane(cT, cnt - 1u);
+      } else if (rmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
+                 __ballot(in && !(cL >= (uint32_t)kMinMatch && ip + (int32_t)cL == chain.E)) == 0 &&
+                 chain.costE + len_extra((uint32_t)(chain.E - h)) <= costNext + 1u + (lits + 1u == litBump ? 1u : 0u)) {
+        // every position of the chunk continues the chain: all take the full length (the first one
+        // beats its literal, the others beat theirs since extra(x + 1) <= extra(x) + 1)
+        const uint32_t cT = chain.costE + len_extra((uint32_t)(chain.E - ip));
+        const uint32_t delta = cT - cC;
+        uint32_t dPrev = __shfl_up(delta, 1, 64);
+        if (lane == 0) dPrev = prevDelta;
+        const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
+        const uint64_t upTo = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
+        const int32_t rt = (chg & upTo) ? h - (63 - (int32_t)__builtin_clzll(chg & upTo)) : runTop;
+        const int32_t need = (int32_t)cR > ip ? (int32_t)cR : ip;
+        const uint64_t cv = __ballot(lane < cnt && cS != 1u && rt >= need);
+        const uint32_t last = cv ? (uint32_t)__builtin_ctzll(cv) : cnt - 1u;  // last position processed
+        if (lane <= last) {
+          S[ip] = cL;
+          cost[ip] = cT;
+          ring[ip & (kRing - 1)] = cT;
+        }
+        const uint32_t tl = ((uint32_t)h - lane) & 63u;
+        if (tl <= last) cbuf = chain.costE + len_extra((uint32_t)(chain.E - (h - (int32_t)tl)));
+        const uint32_t mE = chain.costE + kMarginBias;
+        chain.margin = mE < chain.margin ? mE : chain.margin;
+        runTop = rdlane((uint32_t)rt, last);
+        prevDelta = rdlane(delta, last);
+        costNext = rdlane(cT, last);
+        lits = 0;
+        litBump = 15;
+        if (cv) {
+          conv = h - (int32_t)last;
+          convDelta = prevDelta;
+          done = true;
+        }
+      } else
       for (uint32_t t = 0; t < 64; t++) {
         const int32_t i = h - (int32_t)t;
         if (i < lo) break;
@@ -1457,26 +2312,36 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
             best = Lk;
             minCost = cost_at(i, i + (int32_t)Lk) + 4 + (Lk - 19) / 255;
           } else {
-            const uint32_t len = ((lane - (uint32_t)i - 1u) & 63u) + 1u;
-            const uint32_t top = Lk < 64 ? Lk : 64u;
-            const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
-            const uint32_t kmin = wave_min_fast(len - 4u <= top - 4u ? key : 0xFFFFFFFFu);
-            if ((kmin >> 6) <= minCost) {
-              minCost = kmin >> 6;
-              best = 64u - (kmin & 63u);
-            }
-            for (uint32_t b = 65; b <= Lk; b += 64) {
-              const uint32_t ln = b + lane;
-              uint32_t k2 = 0xFFFFFFFFu;
-              if (ln <= Lk) k2 = ((cost_at(i, i + (int32_t)ln) + len_extra(ln)) << 6) | (63u - lane);
-              const uint32_t km = wave_min_fast(k2);
-              if (km != 0xFFFFFFFFu && (km >> 6) <= minCost) {
-                minCost = km >> 6;
-                best = b + (63u - (km & 63u));
+            auto cost_j = [&](int32_t j) -> uint32_t { return cost_at(i, j); };
+            const int32_t Ei = i + (int32_t)Lk;  // <= top + 1
+            if (rmq && Lk >= kRmqLen && chain.valid && chain.E == Ei && chain.margin + 2u >= chain.costE + kMarginBias) {
+              const uint32_t mc = chain.costE + len_extra(Lk);  // carried match: the full length
+              if (mc <= minCost) {
+                minCost = mc;
+                best = Lk;
+              }
+            } else {
+              const uint32_t len = ((lane - (uint32_t)i - 1u) & 63u) + 1u;
+              const uint32_t lim64 = Lk < 64 ? Lk : 64u;
+              const uint32_t key = ((cbuf + 3u + ((len + 45u) >> 6)) << 6) + (64u - len);
+              const uint32_t kmin = wave_min_fast(len - 4u <= lim64 - 4u ? key : 0xFFFFFFFFu);
+              if ((kmin >> 6) <= minCost) {
+                minCost = kmin >> 6;
+                best = 64u - (kmin & 63u);
+              }
+              if (Lk > 64u) long_lengths(i, Lk, top, top, rmq, up, down, cost_j, key_cost, minCost, best);
+              if (rmq && Lk >= kRmqLen) {
+                chain.E = Ei;
+                chain.costE = Ei > top ? 0u : cost_j(Ei);
+                chain.valid = i == h;
+                chain.pending = i != h;
+                if (i == h) chain.margin = end_margin(i, Ei, top, up, down, cost_j, key_cost);
               }
             }
           }
         }
+        if (Lk >= (uint32_t)kMinMatch && i + (int32_t)Lk == chain.E) chain.add(i, minCost);
+        else chain.valid = chain.pending = false;  // chains are contiguous
         const uint32_t specBest = rdlane(cS, t), specCost = rdlane(cC, t), rch = rdlane(cR, t);
         if (lane == 0) {
           S[i] = best;
@@ -1500,8 +2365,36 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
           }
         }
       }
+      if (rmq) {
+        if (!done) {
+          // UP of the chunk, DOWN of a finished rmq block
+          const uint32_t kt = lane < cnt ? rmq_key(ring[ip & (kRing - 1)], top, ip) : 0xFFFFFFFFu;
+          rmq_store_up(up, top, h, cnt, kt, upCarry);
+          if (cl == 0 || ((uint32_t)(top - cl) & 255u) == 255u)
+            rmq_store_down(down, top, cl, [&](int32_t j) -> uint32_t { return ring[j & (kRing - 1)]; });
+          if (chain.pending) {
+            const int32_t i = cl - 1;
+            auto cost_j = [&](int32_t j) -> uint32_t { return cost_at(i, j); };
+            chain.margin = end_margin(i, chain.E, top, up, down, cost_j, key_cost);
+            chain.valid = true;
+            chain.pending = false;
+          }
+        } else {
+          // converged inside conv's rmq block: its keys again, exact (below conv: stored + delta)
+          const int32_t jt = rmq_block_top(top, conv);
+          const int32_t jb0 = jt - 255;
+          const int32_t jb = jb0 > lo ? jb0 : lo;
+          auto exact = [&](int32_t j) -> uint32_t {
+            return j >= conv ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]) + convDelta;
+          };
+          rmq_store_up_block(up, top, jb, jt, exact);
+          rmq_store_down(down, top, jb, exact);
+          if (lane == 0) convBlk[k] = (uint32_t)jb;
+        }
+      }
     }
     if (lane == 0) {
+      if (!done || !rmq) convBlk[k] = (uint32_t)conv;
       convTab[k] = (uint32_t)conv;
       deltaTab[k] = convDelta;
       // not converged: the state below the segment is this pass's own
@@ -1864,47 +2757,67 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
 }
 
 uint32_t find_lds_bytes() { return 65536 + 16; }
+uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
-                 const uint32_t* ivCount, const uint2* compact, const uint32_t* rank, uint32_t maxChain,
-                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, bool ldsWindow, hipStream_t s)
+                 const uint32_t* ivCount, const uint2* compact, uint2* scratch, const uint32_t* rank, uint32_t maxChain,
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* longBits, uint32_t* segLong,
+                 uint32_t* longFlag, bool ldsWindow, uint32_t hybridLds, hipStream_t s)
 {
   if (!nsegs) return;
+  const bool unlimited = maxChain >= 65535u;
   if (ldsWindow) {
     static bool attr = false;
     if (!attr) {
       hipFuncSetAttribute((const void*)k_find<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       hipFuncSetAttribute((const void*)k_find_sorted<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
+      hipFuncSetAttribute((const void*)k_find_long9<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       attr = true;
     }
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
-                         ivCount, compact, maxChain, mlen, mdist, matchBase);
+                         ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong);
+    else if (unlimited)
+      hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
+                         ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag);
     else
       hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                         compact, rank, maxChain, mlen, mdist, matchBase);
+                         compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
   } else {
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
-                         maxChain, mlen, mdist, matchBase);
+                         maxChain, mlen, mdist, matchBase, longBits, segLong);
+    else if (unlimited) {
+      static uint32_t attrBytes = 0;
+      if (hybridLds > attrBytes) {
+        hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+        attrBytes = hybridLds;
+      }
+      hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+                         compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag);
+    }
     else
       hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
-                         maxChain, mlen, mdist, matchBase);
+                         maxChain, mlen, mdist, matchBase, longFlag);
   }
 }
 
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
-                  uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, int* status, hipStream_t s)
+                  uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, const uint32_t* longFlag, uint32_t* rmqUp,
+                  uint32_t* rmqDown, int* status, hipStream_t s)
 {
   (void)in;
   if (!nblocks) return;
   hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, maxChain, mlen, matchBase, sel, status);
   if (maxChain <= (uint32_t)kGreedyMax || !ndp) return;
-  hipLaunchKernelGGL(k_dp_spec, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs, ndp,
-                     mlen, mdist, matchBase, cost, sel, reach, segState);
+  // every segment is parsed by exactly one of the two instantiations (by its block's longFlag)
+  hipLaunchKernelGGL(k_dp_spec<false>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
+                     ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
+  hipLaunchKernelGGL(k_dp_spec<true>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
+                     ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
   hipLaunchKernelGGL(k_dp_fix, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
-                     segState);
+                     segState, longFlag, rmqUp, rmqDown);
 }
 
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,

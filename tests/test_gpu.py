@@ -34,7 +34,7 @@ def test_blocks_text_every_level(compressor, chain):
     ("runs", synth.runs(400000, seed=4, max_run=5000)),
     ("zeros", bytes(200000)),
     ("zeros_urandom", synth.zeros_urandom(600000, run=70000, seed=5)),
-])
+], ids=lambda v: v if isinstance(v, str) else "")
 @pytest.mark.parametrize("chain", [7, 65535])
 def test_blocks_shapes(compressor, name, data, chain):
     assert compressor.compress_blocks(data, 65536, chain) == expected_frame(data, 65536, chain)
@@ -68,6 +68,20 @@ def test_blocks_headers(compressor):
     assert indep[6] == (xxhash.xxh32(indep[4:6]).intdigest() >> 8) & 0xFF
     assert indep[7:] == full[7:]
     assert pyoracle.oz_unlz4(indep) == data
+
+
+@pytest.mark.parametrize("name,data,bs,chains", [
+    ("repeats64k", synth.repeats(400000, seed=21, unit=20000, mutate_every=3000), 65536, (7, 65535)),
+    ("repeats256k", synth.repeats(600000, seed=22, unit=30000, mutate_every=9000), 262144, (7, 65535)),
+    ("repeats1m", synth.repeats(700000, seed=25, unit=50000, mutate_every=30000), 1 << 20, (65535,)),
+    ("runs256k", synth.runs(300000, seed=23, max_run=20000), 262144, (65535,)),
+    ("zeros_urandom256k", synth.zeros_urandom(262144, seed=24), 262144, (65535,)),
+], ids=lambda v: v if isinstance(v, str) else "")
+def test_blocks_long_matches(compressor, name, data, bs, chains):
+    """Matches of hundreds to tens of thousands of bytes: the parse's range minima (UP/DOWN), the
+    repair pass across parse segments, the finder's early exit and pass-2 seed."""
+    for chain in chains:
+        assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain), chain
 
 
 def test_blocks_long_run_shortcut(compressor):
