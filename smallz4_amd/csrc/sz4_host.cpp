@@ -256,12 +256,12 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if (maxChain > 0)
     launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                 c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                nullptr, c->ldsWindow, c->hybridLds, s);
+                nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, s);
   mark(c, 3, s);
   if (maxChain > 0)
     launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                 c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                c->longFlag.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
+                c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
   mark(c, 4, s);
   if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),

@@ -92,12 +92,13 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
                  uint32_t* rank, hipStream_t s);
 // pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals)
 // scratch: per-slot words free after k_sort (the skip pointers of k_find_long9); longBits: one bit per
-// position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target
+// position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target;
+// specLen/specDist: per position words free before the parse (speculative carries of pass-2 piece heads)
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, const uint2* compact, uint2* scratch,
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
-                 uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, bool ldsWindow, uint32_t hybridLds,
-                 hipStream_t s);
+                 uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
+                 bool ldsWindow, uint32_t hybridLds, hipStream_t s);
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,

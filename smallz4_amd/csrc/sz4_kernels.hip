@@ -1265,7 +1265,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
                                                              uint2* __restrict__ skipAll, const uint32_t* __restrict__ rankAll,
                                                              const uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
                                                              uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                             uint64_t matchBase, uint32_t* __restrict__ longFlag)
+                                                             uint64_t matchBase, uint32_t* __restrict__ longFlag,
+                                                             uint32_t* __restrict__ specLen, uint32_t* __restrict__ specDist,
+                                                             int fixMode)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
@@ -1345,7 +1347,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
 
   // 1. skip[s] = the slot just below the run of equal preceding bytes that holds s (runs end at
   //    group starts): an inclusive max-scan of run starts, tiles of 1024 slots
-  if (searched) {
+  if (searched && !fixMode) {
     uint32_t carry = 0;
     for (uint32_t base = 0; base < E; base += kFindThreads) {
       const uint32_t sl = base + tid;
@@ -1455,6 +1457,47 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
     bDist = bestDist;
   };
 
+  // a stretch from q: best matches one after the other, each carrying into the next; ends at the
+  // piece boundary or the first target pass 1 finished
+  auto walk_stretch = [&](uint64_t q, uint32_t cLen, uint32_t cDist, bool exact) {
+    bool rmqLen = false;
+    uint32_t bits = longBits[(q - matchBase) >> 5];  // this stretch's long bits, a word at a time
+    while (true) {
+      uint32_t bLen, bDist;
+      best_of(q, cLen, cDist, exact, bLen, bDist);
+      if (lane == 0) {
+        mlen[q - matchBase] = bLen;
+        mdist[q - matchBase] = (uint16_t)bDist;
+      }
+      rmqLen |= bLen >= kRmqLen && !(bDist == 1u && bLen >= kSameLetter);
+      cLen = bLen;
+      cDist = bDist;
+      exact = true;
+      q++;
+      if (q >= S.s1 || ((q - S.s0) & (kPiece - 1)) == 0) break;
+      const uint64_t qi = q - matchBase;
+      if ((qi & 31) == 0) bits = longBits[qi >> 5];
+      if (!((bits >> (qi & 31)) & 1u)) break;
+    }
+    if (rmqLen && lane == 0) atomicOr(&longFlag[S.block], 1u);
+  };
+
+  if (fixMode) {
+    // repair pass: piece heads whose predecessor was still unknown walked with a speculative carry
+    // (specLen, specDist).  In text order, a head whose predecessor's final result differs is walked
+    // again with the true carry (which may change the next head's predecessor in turn).
+    if (wave != 0 || !searched) return;
+    for (uint64_t q0 = S.s0 + kPiece; q0 < S.s1; q0 += kPiece) {
+      if (!long_bit(q0) || !long_bit(q0 - 1)) continue;
+      const uint32_t sd = specDist[q0 - matchBase];
+      if (sd == 0u) continue;  // walked without a carry: exact
+      const uint32_t aLen = mlen[q0 - 1 - matchBase], aDist = mdist[q0 - 1 - matchBase];
+      if (aLen == specLen[q0 - matchBase] && aDist == sd) continue;
+      walk_stretch(q0, aLen, aDist, true);
+    }
+    return;
+  }
+
   const uint32_t nTargets = (uint32_t)(S.s1 - S.s0);
   while (true) {
     uint32_t chunkIdx = 0;
@@ -1483,7 +1526,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
     while (heads) {
       const uint32_t h = (uint32_t)__builtin_ctzll(heads);
       heads &= heads - 1;
-      uint64_t q = S.s0 + first + h;
+      const uint64_t q = S.s0 + first + h;
       // p-1's result: final when it is a target of this block that pass 1 finished
       uint32_t cLen = 0, cDist = 0;
       bool exact = false;
@@ -1491,21 +1534,26 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
         cLen = mlen[q - 1 - matchBase];
         cDist = mdist[q - 1 - matchBase];
         exact = true;
-      }
-      while (true) {
-        uint32_t bLen, bDist;
-        best_of(q, cLen, cDist, exact, bLen, bDist);
-        if (lane == 0) {
-          mlen[q - matchBase] = bLen;
-          mdist[q - matchBase] = (uint16_t)bDist;
-          if (bLen >= kRmqLen && !(bDist == 1u && bLen >= kSameLetter)) atomicOr(&longFlag[S.block], 1u);
+      } else if (q != S.s0 && long_bit(q - 1) && cut == kNone) {
+        // a piece head inside a stretch: speculate that its predecessor's best match is the one
+        // that makes the nearest candidate its carry (checked and repaired by the fixMode pass)
+        const uint32_t key = src.ld4(q);
+        const uint32_t slot = rank[q - S.s0];
+        const int32_t gs = (int32_t)slot_gs(compact, small, E, slot);
+        if ((int32_t)slot - 1 >= gs) {
+          const uint64_t c = S.w0 + slot_pos(compact, small, slot - 1);
+          if (c + kWindow >= q && src.ld4(c) == key && !excluded(c)) {
+            cLen = wave_exact_prefix(src, q, c, (uint32_t)(stopAbs - q)) + 1u;
+            cDist = (uint32_t)(q - c);
+            exact = true;
+          }
         }
-        cLen = bLen;
-        cDist = bDist;
-        exact = true;
-        q++;
-        if (q >= S.s1 || ((q - S.s0) & (kPiece - 1)) == 0 || !long_bit(q)) break;
       }
+      if (lane == 0 && q != S.s0 && long_bit(q - 1)) {
+        specLen[q - matchBase] = cLen;
+        specDist[q - matchBase] = exact ? cDist : 0u;
+      }
+      walk_stretch(q, cLen, cDist, exact);
     }
   }
 }
@@ -1976,6 +2024,28 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
       // next window: lane l = cost[lo + l] (position lo + l is lane cnt - 1 - l; only a full chunk has a next)
       win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((63u - lane) << 2), (int)mcBuf) << 6;
       chain.valid = chain.pending = false;
+    } else if (__ballot(lane < cnt && myL >= kSameLetter) == (cnt == 64u ? ~0ull : ((1ull << cnt) - 1ull)) &&
+               [&]() -> bool {
+                 const int32_t i = hi - (int32_t)lane;
+                 const int32_t E0 = hi + (int32_t)rdlane(myL, 0);
+                 const bool ok = lane >= cnt || (D[i] == 1u && i + (int32_t)myL == E0);
+                 return __ballot(!ok) == 0;
+               }()) {
+      // a same-letter run: every position takes its distance-1 match unconditionally (smallz4.h:413-419)
+      const int32_t i = hi - (int32_t)lane;
+      const int32_t E0 = hi + (int32_t)rdlane(myL, 0);
+      const uint32_t cE = E0 > segHi ? 0u : (E0 - hi < kRing - 64 ? ring[E0 & (kRing - 1)] : ld_fresh(&cost[E0]));
+      mcBuf = cE + 4u + (myL - 19u) / 255u;
+      kvBuf = 0;
+      bestBuf = myL;
+      (void)i;
+      costNext = rdlane(mcBuf, cnt - 1u);
+      lits = 0;
+      litBump = 15;
+      if constexpr (kRmq) {
+        if (E0 != chain.E || E0 > segHi) chain.valid = chain.pending = false;
+      }
+      win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((63u - lane) << 2), (int)mcBuf) << 6;
     } else if (kRmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
                [&]() -> bool {
                  // every position continues the chain (a same-letter run position only when its end
@@ -2226,6 +2296,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     uint32_t convDelta = 0;
     uint32_t upCarry = 0xFFFFFFFFu;
     RunEnd chain;
+    uint32_t closedCost = 0;  // closed-form chunk: cost at its end closedE
+    int32_t closedE = 0;
     bool done = false;
     for (int32_t h = hi; h >= lo && !done; h -= 64) {
       const int32_t ip = h - (int32_t)lane;
@@ -2261,12 +2333,28 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         lits += cnt;
         litBump += 255u * rdlane(nb, cnt - 1u);
         costNext = rdlane(cT, cnt - 1u);
-      } else if (rmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
-                 __ballot(in && !(cL >= (uint32_t)kMinMatch && ip + (int32_t)cL == chain.E)) == 0 &&
-                 chain.costE + len_extra((uint32_t)(chain.E - h)) <= costNext + 1u + (lits + 1u == litBump ? 1u : 0u)) {
-        // every position of the chunk continues the chain: all take the full length (the first one
-        // beats its literal, the others beat theirs since extra(x + 1) <= extra(x) + 1)
-        const uint32_t cT = chain.costE + len_extra((uint32_t)(chain.E - ip));
+      } else if ([&]() -> bool {
+                   // closed-form chunks: (a) a same-letter run, every position taking its distance-1
+                   // match unconditionally (smallz4.h:413-419); (b) a carried chain whose full lengths
+                   // are optimal (the first one beats its literal, the others beat theirs since
+                   // extra(x + 1) <= extra(x) + 1)
+                   const int32_t E0 = h + (int32_t)rdlane(cL, 0);
+                   if (__ballot(in && !(cL >= kSameLetter && cD == 1u && ip + (int32_t)cL == E0)) == 0) {
+                     closedCost = cost_at(h, E0);
+                     closedE = E0;
+                     return true;
+                   }
+                   if (rmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
+                       __ballot(in && !(cL >= (uint32_t)kMinMatch && ip + (int32_t)cL == chain.E)) == 0 &&
+                       chain.costE + len_extra((uint32_t)(chain.E - h)) <= costNext + 1u + (lits + 1u == litBump ? 1u : 0u)) {
+                     closedCost = chain.costE;
+                     closedE = chain.E;
+                     return true;
+                   }
+                   return false;
+                 }()) {
+        const uint32_t cT = closedCost + len_extra((uint32_t)(closedE - ip));
+        if (closedE != chain.E) chain.valid = chain.pending = false;
         const uint32_t delta = cT - cC;
         uint32_t dPrev = __shfl_up(delta, 1, 64);
         if (lane == 0) dPrev = prevDelta;
@@ -2282,9 +2370,9 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
           ring[ip & (kRing - 1)] = cT;
         }
         const uint32_t tl = ((uint32_t)h - lane) & 63u;
-        if (tl <= last) cbuf = chain.costE + len_extra((uint32_t)(chain.E - (h - (int32_t)tl)));
-        const uint32_t mE = chain.costE + kMarginBias;
-        chain.margin = mE < chain.margin ? mE : chain.margin;
+        if (tl <= last) cbuf = closedCost + len_extra((uint32_t)(closedE - (h - (int32_t)tl)));
+        const uint32_t mE = closedCost + kMarginBias;
+        if (chain.valid) chain.margin = mE < chain.margin ? mE : chain.margin;
         runTop = rdlane((uint32_t)rt, last);
         prevDelta = rdlane(delta, last);
         costNext = rdlane(cT, last);
@@ -2654,6 +2742,8 @@ __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ bloc
   if (tid == 0) offsets[nblocks] = s_carry;
 }
 
+constexpr uint64_t kOwnLits = 64;  // longer literal runs are copied by the whole workgroup
+
 // k_write: one 256-thread workgroup per block writes the block word and either the raw bytes
 // (stored block) or its tokens: token offsets by a workgroup scan of token sizes, then every
 // thread encodes one token (smallz4.h:310-367) straight into the frame.
@@ -2664,6 +2754,8 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
 {
   __shared__ uint64_t s_w[4];
   __shared__ uint64_t s_carry;
+  __shared__ uint32_t s_nLong;
+  __shared__ uint32_t s_longDst[256], s_longSrc[256], s_longLen[256];  // long literal runs of one round
   const Block B = blocks[blockIdx.x];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t bb = blockBytes[blockIdx.x];
@@ -2688,6 +2780,7 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
   const uint32_t ntok = ntokAll[blockIdx.x];
   __syncthreads();
   for (uint32_t base = 0; base < ntok; base += 256) {
+    if (tid == 0) s_nLong = 0;
     const uint32_t t = base + tid;
     Token T{0, 0, 0, 0};
     uint64_t sz = 0;
@@ -2723,7 +2816,15 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
         *o++ = (uint8_t)v;
       }
       const uint8_t* ls = src + T.litFrom;
-      for (uint64_t k = 0; k < lits; k++) o[k] = ls[k];
+      if (lits <= kOwnLits) {
+        for (uint64_t k = 0; k < lits; k++) o[k] = ls[k];
+      } else {
+        // copied by the whole workgroup below
+        const uint32_t slot = atomicAdd(&s_nLong, 1u);
+        s_longDst[slot] = (uint32_t)(o - dst);
+        s_longSrc[slot] = T.litFrom;
+        s_longLen[slot] = (uint32_t)lits;
+      }
       o += lits;
       if (!last) {
         const uint32_t dd = T.dist & 0xFFFFu;
@@ -2736,6 +2837,12 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
           *o++ = (uint8_t)v;
         }
       }
+    }
+    __syncthreads();
+    for (uint32_t r = 0; r < s_nLong; r++) {
+      uint8_t* d = dst + s_longDst[r];
+      const uint8_t* ls = src + s_longSrc[r];
+      for (uint32_t k = tid; k < s_longLen[r]; k += 256) d[k] = ls[k];
     }
     __syncthreads();
   }
@@ -2762,7 +2869,8 @@ uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
                  const uint32_t* ivCount, const uint2* compact, uint2* scratch, const uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* longBits, uint32_t* segLong,
-                 uint32_t* longFlag, bool ldsWindow, uint32_t hybridLds, hipStream_t s)
+                 uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist, bool ldsWindow, uint32_t hybridLds,
+                 hipStream_t s)
 {
   if (!nsegs) return;
   const bool unlimited = maxChain >= 65535u;
@@ -2778,8 +2886,10 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                          ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong);
     else if (unlimited)
-      hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
-                         ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag);
+      for (int fix = 0; fix < 2; fix++)
+        hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
+                           ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
+                           specDist, fix);
     else
       hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
                          compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
@@ -2793,8 +2903,10 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
         hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
         attrBytes = hybridLds;
       }
-      hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
-                         compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag);
+      for (int fix = 0; fix < 2; fix++)
+        hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+                           compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen, specDist,
+                           fix);
     }
     else
       hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
