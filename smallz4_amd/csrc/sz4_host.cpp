@@ -245,25 +245,39 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   mark(c, 0, s);
   launch_runs(in, dB, nb, dIv, dIvN, s);
   mark(c, 1, s);
-  if (maxChain > 0) {
-    launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
-    // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
-    if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
-        (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
-      return c->fail(SZ4_E_DEVICE, "clear matches", e);
+  // greedy/lazy levels: k_prep verifies the shortcut intervals k_runs assumed; a corrected block needs
+  // another sort/find/prep round (each round checks a longer prefix of it)
+  for (uint32_t round = 0;; round++) {
+    if (maxChain > 0) {
+      launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
+      // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
+      if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
+          (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
+        return c->fail(SZ4_E_DEVICE, "clear matches", e);
+    }
+    mark(c, 2, s);
+    if (maxChain > 0)
+      launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                  c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
+                  nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, s);
+    mark(c, 3, s);
+    if (maxChain > 0)
+      launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+                  c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
+                  c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
+    mark(c, 4, s);
+    if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
+    launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel.as<uint32_t>(),
+                c->status.as<int>(), s);
+    if (maxChain == 0 || maxChain > (uint32_t)kLazyMax) break;
+    int st = 0;
+    if ((e = hipMemcpyAsync(&st, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "prep", e);
+    if (!(st & 2)) break;
+    if (round > 2 * kMaxIv + 2) return c->fail(SZ4_E_DEVICE, "shortcut intervals did not settle");
+    if ((e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
+      return c->fail(SZ4_E_DEVICE, "prep", e);
   }
-  mark(c, 2, s);
-  if (maxChain > 0)
-    launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, s);
-  mark(c, 3, s);
-  if (maxChain > 0)
-    launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
-  mark(c, 4, s);
-  if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
                c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp.as<uint32_t>(), c->rmqDown.as<uint32_t>(),
@@ -284,7 +298,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if ((e = hipMemcpyAsync(&total, c->offsets.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s)) ||
       (e = hipMemcpyAsync(&status, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
     return c->fail(SZ4_E_DEVICE, "pipeline", e);
-  if (status) return c->fail(SZ4_E_UNSUPPORTED, "greedy/lazy level on a block with a same-letter run > 65299 bytes");
+  (void)status;
   const uint64_t size = hdrLen + total + (endMark ? 4 : 0);
   if (size > outCap) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
   if (hdrLen && (e = hipMemcpyAsync(out, hdr, hdrLen, hipMemcpyHostToDevice, s)))

@@ -99,6 +99,10 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
                  bool ldsWindow, uint32_t hybridLds, hipStream_t s);
+// k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
+// corrected, run sort/find/prep again
+void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, int* status, hipStream_t s);
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,

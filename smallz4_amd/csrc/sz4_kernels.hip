@@ -154,6 +154,30 @@ __device__ __forceinline__ uint32_t wave_min_all(uint32_t v)
   return min(b[0], b[1]);
 }
 
+// four wave-wide minima, interleaved so that no DPP step waits on the one before (no s_nop), rows
+// joined with permlane swaps; results uniform
+__device__ __forceinline__ void wave_min4(uint32_t (&v)[4])
+{
+#pragma unroll
+  for (int r = 0; r < 4; r++) v[r] = min(v[r], dpp<kQuadSwap1>(v[r]));
+#pragma unroll
+  for (int r = 0; r < 4; r++) v[r] = min(v[r], dpp<kQuadSwap2>(v[r]));
+#pragma unroll
+  for (int r = 0; r < 4; r++) v[r] = min(v[r], dpp<kRowHalfMirror>(v[r]));
+#pragma unroll
+  for (int r = 0; r < 4; r++) v[r] = min(v[r], dpp<kRowMirror>(v[r]));
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    auto a = __builtin_amdgcn_permlane16_swap(v[r], v[r], false, false);
+    v[r] = min(a[0], a[1]);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    auto b = __builtin_amdgcn_permlane32_swap(v[r], v[r], false, false);
+    v[r] = (uint32_t)__builtin_amdgcn_readfirstlane((int)min(b[0], b[1]));
+  }
+}
+
 // wave-wide min, result uniform
 __device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
 {
@@ -1874,14 +1898,23 @@ struct RunEnd {
   }
 };
 
-__global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, const uint32_t* __restrict__ ivCount,
-                                             uint32_t maxChain, uint32_t* __restrict__ mlen, uint64_t matchBase,
-                                             uint32_t* __restrict__ sel, int* __restrict__ status)
+// Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut
+// starts depends on the skip state (smallz4.h:631-643, 726-744): the interval k_runs assumed (the
+// run's first position) may start later, or not at all.  k_prep replays the reference's loop in order
+// -- self-match check first, then the skip bookkeeping -- and compares every shortcut position with
+// the assumed intervals.  At the first disagreement it corrects that interval (later positions were
+// searched against the wrong chains) and asks the host for another sort/find/prep round; the checked
+// prefix grows every round.
+__global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                             Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount,
+                                             uint32_t maxChain, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                             uint64_t matchBase, uint32_t* __restrict__ sel, int* __restrict__ status)
 {
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const uint64_t n = B.end - B.start;
   uint32_t* L = mlen + (B.start - matchBase);
+  uint16_t* D = mdist + (B.start - matchBase);
   uint32_t* S = sel + (B.start - matchBase);
   if (maxChain == 0) return;
   const uint64_t lastSearch = n >= (uint64_t)kTailNoMatch ? n - kTailNoMatch : 0;  // inclusive, relative
@@ -1894,39 +1927,101 @@ __global__ __launch_bounds__(64) void k_prep(const Block* __restrict__ blocks, c
     for (uint64_t i = from + lane; i < n; i += 64) S[i] = 0;
   }
   if (maxChain > (uint32_t)kLazyMax || n < (uint64_t)kTailNoMatch) return;
-  if (ivCount[blockIdx.x] && lane == 0) atomicOr(status, 1);  // shortcut interplay with skipping: not on this path
 
-  // one lane replays the reference's bookkeeping over an LDS copy of each 64-position chunk
+  // one lane replays the reference's loop over an LDS copy of each 64-position chunk
   __shared__ uint32_t chunkL[64];
+  __shared__ uint16_t chunkD[64];
+  __shared__ uint8_t chunkB[68];  // bytes c0 - 1 .. c0 + 63
+  __shared__ int s_stop;
+  Interval* iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
+  const uint32_t niv = ivCount[blockIdx.x];
+  if (lane == 0) s_stop = 0;
   uint64_t skip = 0;
   bool lazyEval = false;
+  uint32_t prevL = 0, prevD = 0, k0 = 0;  // previous position's match; first interval not yet passed
   for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
     const uint64_t i = c0 + lane;
     const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
     chunkL[lane] = i <= lastSearch ? L[i] : 0u;
+    chunkD[lane] = i <= lastSearch ? D[i] : (uint16_t)0;
+    chunkB[lane + 1] = in[B.start + i];
+    if (lane == 0) chunkB[0] = c0 > 0 ? in[B.start + c0 - 1] : 0;
     __syncthreads();
     if (lane == 0) {
       for (uint32_t k = 0; k < cnt; k++) {
-        const uint32_t lk = chunkL[k];
-        // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
-        if (lk >= (uint32_t)kMinMatch) {
-          bool search = true;
-          if (skip > 0) {
-            skip--;
-            search = lazyEval;  // a pending lazy evaluation searches one more position
-            lazyEval = false;
-          }
-          if (search) {
-            lazyEval = (skip == 0);
-            skip = lk;
+        const uint64_t pos = c0 + k, abs = B.start + pos;
+        while (k0 < niv && iv[k0].hi <= abs) k0++;
+        const bool assumed = k0 < niv && abs >= iv[k0].lo;
+        // self-matching (smallz4.h:631-643): the predecessor's distance-1 match, one shorter
+        const bool sc = pos > 0 && chunkB[k + 1] == chunkB[k] && prevD == 1u && prevL > kSameLetter;
+        if (sc != assumed) {
+          // intervals [0, k0) end before this position and were confirmed; the list is edited in place
+          uint32_t m;
+          if (sc) {
+            // a shortcut nobody assumed: it runs while the copied length stays above MaxSameLetter;
+            // it replaces the assumed intervals it overlaps
+            Interval x;
+            x.lo = abs;
+            x.hi = abs + (prevL - kSameLetter);
+            x.a = abs - 1;
+            x.La = prevL;
+            uint32_t r = k0;
+            while (r < niv && iv[r].lo < x.hi) r++;
+            if (r == k0) {
+              for (uint32_t j = niv < kMaxIv ? niv : kMaxIv - 1; j > k0; j--) iv[j] = iv[j - 1];
+              m = niv < kMaxIv ? niv + 1 : kMaxIv;
+            } else {
+              for (uint32_t j = 0; j < niv - r; j++) iv[k0 + 1 + j] = iv[r + j];
+              m = k0 + 1 + (niv - r);
+            }
+            iv[k0] = x;
           } else {
-            chunkL[k] = 0;  // never searched by the reference
+            // an assumed shortcut that does not happen here: dropped (a later position of the run may
+            // start the real one, found in the next round)
+            for (uint32_t j = k0; j + 1 < niv; j++) iv[j] = iv[j + 1];
+            m = niv - 1;
+          }
+          ivCount[blockIdx.x] = m;
+          atomicOr(status, 2);
+          s_stop = 1;
+          break;
+        }
+        uint32_t curL = 0, curD = 0;
+        if (sc) {
+          curL = prevL - 1;
+          curD = 1;
+          chunkL[k] = curL;
+          chunkD[k] = 1;
+        } else {
+          const uint32_t lk = chunkL[k];
+          // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
+          if (lk >= (uint32_t)kMinMatch) {
+            bool search = true;
+            if (skip > 0) {
+              skip--;
+              search = lazyEval;  // a pending lazy evaluation searches one more position
+              lazyEval = false;
+            }
+            if (search) {
+              lazyEval = (skip == 0);
+              skip = lk;
+              curL = lk;
+              curD = chunkD[k];
+            } else {
+              chunkL[k] = 0;  // never searched by the reference
+            }
           }
         }
+        prevL = curL;
+        prevD = curD;
       }
     }
     __syncthreads();
-    if (i <= lastSearch) L[i] = chunkL[lane];
+    if (s_stop) return;  // another round recomputes this block
+    if (i <= lastSearch) {
+      L[i] = chunkL[lane];
+      D[i] = chunkD[lane];
+    }
     __syncthreads();
   }
 }
@@ -2095,8 +2190,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
 #pragma unroll
         for (int r = 0; r < 4; r++) kv[r] = rdlane(row_min(kv[r]), 0);
       } else {
-#pragma unroll
-        for (int r = 0; r < 4; r++) kv[r] = wave_min_fast(kv[r]);
+        wave_min4(kv);
       }
       // fast batch: four whole positions, no literal-length bump reachable, no length beyond 64
       if (i0 - 3 >= lo && maxL <= 64u && lits + 4u < litBump) {
@@ -2914,6 +3008,14 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
   }
 }
 
+void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, int* status, hipStream_t s)
+{
+  if (nblocks)
+    hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, in, blocks, iv, ivCount, maxChain, mlen, mdist, matchBase, sel,
+                       status);
+}
+
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
                   uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, const uint32_t* longFlag, uint32_t* rmqUp,
@@ -2921,7 +3023,6 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
 {
   (void)in;
   if (!nblocks) return;
-  hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, maxChain, mlen, matchBase, sel, status);
   if (maxChain <= (uint32_t)kGreedyMax || !ndp) return;
   // every segment is parsed by exactly one of the two instantiations (by its block's longFlag)
   hipLaunchKernelGGL(k_dp_spec<false>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,

@@ -84,6 +84,25 @@ def test_blocks_long_matches(compressor, name, data, bs, chains):
         assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain), chain
 
 
+def _skip_into_run(seed):
+    """A long match that ends 10 bytes into a 100 KB zero run: at greedy/lazy levels the run's first
+    positions are skipped, so the same-letter shortcut starts later than the run."""
+    rng = np.random.default_rng(seed)
+    r = rng.integers(1, 256, size=1000, dtype=np.uint8).tobytes()
+    return synth.enwik8_like(3000, seed=seed) + r + bytes(10) + b"xyz" + r + bytes(100000) + synth.enwik8_like(20000, seed=seed + 1)
+
+
+@pytest.mark.parametrize("chain", [1, 2, 3, 4, 5, 6])
+def test_greedy_lazy_long_runs(compressor, chain):
+    """Greedy/lazy levels on same-letter runs > 65299 bytes: k_prep verifies the assumed shortcut
+    intervals and the pipeline reruns until they match the reference's loop (smallz4.h:631-643, 726-744)."""
+    for data, bs in ((_skip_into_run(40), 262144), (synth.enwik8_like(30000, seed=41) + bytes(150000), 262144),
+                     (bytes(70000) + synth.enwik8_like(5000, seed=42) + bytes(90000), 1 << 20)):
+        assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain)
+    data = synth.enwik8_like((4 << 20) - 40000, seed=43) + bytes(140000) + synth.enwik8_like(10000, seed=44)
+    assert compressor.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
+
+
 def test_blocks_long_run_shortcut(compressor):
     # a same-letter run longer than MaxSameLetter inside one 256 KiB block (smallz4.h:631-643)
     data = synth.enwik8_like(30000, seed=9) + bytes(150000) + synth.enwik8_like(82144, seed=10)
@@ -141,12 +160,7 @@ def test_golden_vectors_on_gpu(compressor, golden):
         data = inputs.make(case["input"])
         if "dict" in case:
             continue  # dictionary mode: see test_dictionary_mode_unsupported
-        try:
-            frame = compressor.lz4(data, case["level"], b"", bool(case["legacy"]))
-        except Exception as e:  # greedy/lazy + same-letter run is not on the device path yet
-            if "same-letter" in str(e) and case["level"] <= 6:
-                continue
-            raise
+        frame = compressor.lz4(data, case["level"], b"", bool(case["legacy"]))
         assert inputs.sha(frame) == case["out_sha256"], (case["name"], case["level"], case["legacy"])
 
 
