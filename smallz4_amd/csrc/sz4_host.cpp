@@ -89,6 +89,9 @@ struct sz4_ctx {
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
+  DevBuf dictLast, dictPrevH;  // dictionary mode: the reference's hash table and hash chain
+  int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
+  int dictLegacy = 0;
 
   std::vector<Block> hBlocks;
   std::vector<Segment> hSegs;
@@ -243,11 +246,23 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   uint32_t* dIvN = c->ivCount.as<uint32_t>();
 
   mark(c, 0, s);
-  launch_runs(in, dB, nb, dIv, dIvN, s);
+  if (c->dictBack < 0) launch_runs(in, dB, nb, dIv, dIvN, s);
   mark(c, 1, s);
+  if (c->dictBack >= 0 && maxChain > 0) {
+    // dictionary mode: the reference's sequential match loop (k_dict_matches), then the usual parse
+    if ((e = c->dictLast.reserve(sizeof(uint32_t) << 20)) || (e = c->dictPrevH.reserve(2 * 65536)))
+      return c->fail(SZ4_E_NOMEM, "dictionary tables", e);
+    launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
+                c->dictPrevH.as<uint16_t>(), c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(),
+                c->longFlag.as<uint32_t>(), s);
+    mark(c, 2, s);
+    mark(c, 3, s);
+    mark(c, 4, s);
+    if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
+  }
   // greedy/lazy levels: k_prep verifies the shortcut intervals k_runs assumed; a corrected block needs
   // another sort/find/prep round (each round checks a longer prefix of it)
-  for (uint32_t round = 0;; round++) {
+  for (uint32_t round = 0; c->dictBack < 0; round++) {
     if (maxChain > 0) {
       launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
       // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
@@ -343,7 +358,7 @@ void sz4_destroy(sz4_ctx* c)
   for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
                     &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
                     &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState, &c->longFlag,
-                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong})
+                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong, &c->dictLast, &c->dictPrevH})
     b->release();
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -375,6 +390,7 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   if (out_cap < sz4_bound(n, block_size)) return c->fail(SZ4_E_CAPACITY, "out_cap < sz4_bound(n, block_size)");
   hipSetDevice(c->device);
   hipStream_t s = (hipStream_t)stream;
+  c->dictBack = -1;
   if (c->planN != n || c->planBS != block_size) {
     c->hBlocks.clear();
     for (uint64_t st = 0; st < n; st += block_size) {
@@ -443,24 +459,28 @@ int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const vo
   if (!c || !out_size || (!in && n) || !out || max_chain > 65535 || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
   c->err.clear();
-  if (dict_len) return c->fail(SZ4_E_UNSUPPORTED, "dictionary mode is not implemented on the device yet");
   hipSetDevice(c->device);
   hipStream_t s = nullptr;
+  // dictionary: the staged stream is the reference's data buffer, a 65535-byte prefix (the dictionary's
+  // last bytes, zero-padded in front) and then the input (smallz4.h:554-571)
+  const uint64_t pre = dict_len ? kWindow : 0;
+  c->dictBack = dict_len ? (int64_t)std::min<uint64_t>(dict_len, kWindow) : -1;
+  c->dictLegacy = legacy;
   // block structure of smallz4::compress (smallz4.h:541-606, 614-624, 782-805)
   const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
   c->hBlocks.clear();
   for (uint64_t st = 0; st < n; st += bs) {
     Block B{};
-    B.start = st;
-    B.end = std::min(st + bs, n);
+    B.start = pre + st;
+    B.end = pre + std::min(st + bs, n);
     const bool first = st == 0;
     if (legacy || first) {
-      B.low = st;
+      B.low = B.start;
       B.cut = kNone;
       B.prev = kNoBlock;
     } else {
-      B.low = st - kWindow;
-      B.cut = st - kTailNoMatch;  // re-inserted by the lookback of the next block
+      B.low = B.start - kWindow;
+      B.cut = B.start - kTailNoMatch;  // re-inserted by the lookback of the next block
       B.prev = (uint32_t)c->hBlocks.size() - 1;
     }
     B.flags = legacy ? kBlkLegacy : 0;
@@ -468,17 +488,26 @@ int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const vo
   }
   finish_plan(c);
   c->planN = ~0ull;  // invalidate the independent-block plan cache
-  if (int r = reserve_all(c, n + kPad)) return r;
+  if (int r = reserve_all(c, pre + n + kPad)) return r;
   hipError_t e;
-  if ((e = c->staged.reserve(n + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
+  if ((e = c->staged.reserve(pre + n + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
   DevBuf dout;
   const uint64_t cap = sz4_lz4_bound(n, legacy);
   if ((e = dout.reserve(cap))) return c->fail(SZ4_E_NOMEM, "output", e);
-  if (n && (e = hipMemcpy(c->staged.p, in, n, hipMemcpyHostToDevice))) {
+  if (pre) {
+    std::vector<uint8_t> prefix(pre, 0);
+    const uint64_t k = std::min<uint64_t>(dict_len, pre);
+    memcpy(prefix.data() + pre - k, (const uint8_t*)dict + dict_len - k, k);
+    if ((e = hipMemcpy(c->staged.p, prefix.data(), pre, hipMemcpyHostToDevice))) {
+      dout.release();
+      return c->fail(SZ4_E_DEVICE, "upload", e);
+    }
+  }
+  if (n && (e = hipMemcpy(c->staged.as<uint8_t>() + pre, in, n, hipMemcpyHostToDevice))) {
     dout.release();
     return c->fail(SZ4_E_DEVICE, "upload", e);
   }
-  hipMemset(c->staged.as<uint8_t>() + n, 0, kPad);
+  hipMemset(c->staged.as<uint8_t>() + pre + n, 0, kPad);
   const uint8_t hm[7] = {0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF};
   const uint8_t hl[4] = {0x02, 0x21, 0x4C, 0x18};
   uint64_t size = 0;

@@ -99,6 +99,11 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                  const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
                  bool ldsWindow, uint32_t hybridLds, hipStream_t s);
+// dictionary mode: one wavefront replays the reference's match loop (dictBack = first insertion offset
+// before the first block); last: 2^20 u32 scratch, prevH: 65536 u16 scratch
+void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
+                 uint32_t* last, uint16_t* prevH, uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag,
+                 hipStream_t s);
 // k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
 // corrected, run sort/find/prep again
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,

@@ -1898,6 +1898,162 @@ struct RunEnd {
   }
 };
 
+// ================================================================================================
+// k_dict_matches: dictionary mode (smallz4.h:541-760 with a dictionary).  The reference writes chain
+// entries at block-relative slots (smallz4.h:656) but reads them at absolute ones (smallz4.h:190, 200,
+// 694); with a dictionary every block starts at 65535 mod 65536, so a read finds the neighbour's
+// entry and the chains are no longer same-key runs: the candidates follow a
+// pointer chase the sorted-group model cannot express.  One wavefront replays the reference's loop
+// exactly -- insertions in order, the chain walks, the same-letter shortcut and the greedy/lazy skip
+// -- and writes the same match arrays the data-parallel finders write; the parse and the frame
+// assembly then run as for any stream.  Sequential by nature (and slow): this mode exists for parity.
+// Staged coordinates are the reference's data coordinates: a 65535-byte prefix (dictionary tail,
+// zero-padded in front), then the input.
+// ================================================================================================
+constexpr uint32_t kNoPos = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                                     uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
+                                                     uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
+                                                     uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
+{
+  __shared__ uint16_t prevX[65536];
+  const uint32_t lane = threadIdx.x;
+  auto reset = [&]() {
+    for (uint32_t j = lane; j < 65536; j += 64) {
+      prevX[j] = 0;
+      prevH[j] = 0;
+    }
+    for (uint32_t j = lane; j < (1u << kHashBits); j += 64) last[j] = kNoPos;
+  };
+  reset();
+  for (uint32_t b = 0; b < nblocks; b++) {
+    const Block B = blocks[b];
+    for (uint64_t i = B.start + lane; i < B.end; i += 64) {
+      mlen[i] = 0;
+      mdist[i] = 0;
+      if (maxChain > (uint32_t)kGreedyMax && i + kTailLiterals >= B.end) sel[i] = 0;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (lane != 0) return;
+
+  const bool greedy = maxChain <= (uint32_t)kGreedyMax, lazy = !greedy && maxChain <= (uint32_t)kLazyMax;
+  uint64_t low = 0;  // reference dataZero
+  bool withDict = true;
+  for (uint32_t b = 0; b < nblocks; b++) {
+    const Block B = blocks[b];
+    const uint64_t start = B.start, size = B.end - B.start, stop = B.end - kTailLiterals;
+    int64_t back = withDict ? -(int64_t)dictBack : -(int64_t)(low < (uint64_t)kTailNoMatch ? low : (uint64_t)kTailNoMatch);
+    if (legacy) back = 0;
+    uint64_t skip = 0;
+    bool lazyEval = false, rmq = false;
+    for (int64_t i = back; i + kTailNoMatch <= (int64_t)size; i++) {
+      const uint64_t pos = start + (uint64_t)i;
+      // self-matching (smallz4.h:631-643)
+      if (i > 0 && in[pos] == in[pos - 1] && mdist[pos - 1] == 1 && mlen[pos - 1] > kSameLetter) {
+        mdist[pos] = 1;
+        mlen[pos] = mlen[pos - 1] - 1;
+        continue;
+      }
+      // insertion into both chains (smallz4.h:645-720): written at the block-relative slot
+      const uint32_t slot = (uint32_t)((uint64_t)i & kWindow);
+      const uint32_t four = gload4(in, pos);
+      const uint32_t h = ref_hash(four);
+      uint64_t cand = last[h] == kNoPos ? kNone : (uint64_t)last[h];
+      last[h] = (uint32_t)pos;
+      bool linked = false;
+      if (cand == kNone || pos - cand > kWindow) {
+        prevH[slot] = 0;
+        prevX[slot] = 0;
+      } else {
+        uint64_t dist = pos - cand;
+        prevH[slot] = (uint16_t)dist;
+        bool ok = true;
+        while (true) {
+          if (cand < low) { ok = false; break; }  // the reference would read before its buffer
+          const uint32_t seen = gload4(in, cand);
+          if (seen == four) break;
+          if (ref_hash(seen) != h) { ok = false; break; }
+          const uint16_t step = prevH[cand & kWindow];  // read at the absolute slot
+          if (step == 0) { ok = false; break; }
+          dist += step;
+          if (dist > kWindow) { ok = false; break; }
+          cand -= step;
+          if (cand < low) { ok = false; break; }
+        }
+        prevX[slot] = ok ? (uint16_t)dist : (uint16_t)0;
+        linked = ok && dist != 0;
+      }
+      if (!linked || i < 0) continue;
+      if (skip > 0) {
+        skip--;
+        if (!lazyEval) continue;
+        lazyEval = false;
+      }
+      // findLongestMatch (smallz4.h:173-255): strictly longer replaces, maxChain counts replacements
+      uint64_t bestLen = 1;
+      uint32_t bestDist = 0, steps = maxChain;
+      uint32_t hop = prevX[pos & kWindow];
+      uint64_t backDist = 0;
+      const int64_t room = (int64_t)(stop - pos);
+      while (hop != 0) {
+        backDist += hop;
+        if (backDist > kWindow) break;
+        hop = prevX[(pos - backDist) & kWindow];
+        const int64_t need = (int64_t)bestLen + 1;
+        if (need > room) break;
+        const uint64_t c = pos - backDist;
+        int64_t lo = need - 4;
+        while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
+        if (lo > 0) continue;
+        int64_t hi = need;
+        while (hi + 4 <= room && gload4(in, pos + hi) == gload4(in, c + hi)) hi += 4;
+        while (hi < room && in[pos + hi] == in[c + hi]) hi++;
+        bestLen = (uint64_t)hi;
+        bestDist = (uint32_t)backDist;
+        if (--steps == 0) break;
+      }
+      mlen[pos] = (uint32_t)bestLen;
+      mdist[pos] = (uint16_t)bestDist;
+      rmq |= bestLen >= kRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
+      if ((lazy || greedy) && bestLen != 1) {
+        lazyEval = skip == 0;
+        skip = bestLen;
+      }
+    }
+    // positions the reference searched and found nothing keep (1, 0): the parse reads them as literals
+    longFlag[b] = rmq ? 1u : 0u;
+    withDict = false;
+    if (legacy) {
+      low = B.end;
+      for (uint32_t j = 0; j < 65536; j++) {
+        prevX[j] = 0;
+        prevH[j] = 0;
+      }
+      for (uint32_t j = 0; j < (1u << kHashBits); j++) last[j] = kNoPos;
+    } else if (B.end - low > kWindow) {
+      low = B.end - kWindow;  // the reference keeps only the last 64 KiB - 1 (smallz4.h:799-804)
+    }
+  }
+}
+
+void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
+                 uint32_t* last, uint16_t* prevH, uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag,
+                 hipStream_t s)
+{
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)k_dict_matches, hipFuncAttributeMaxDynamicSharedMemorySize, 0);
+    attr = true;
+  }
+  if (nblocks)
+    hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, legacy, last, prevH,
+                       mlen, mdist, sel, longFlag);
+}
+
 // Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut
 // starts depends on the skip state (smallz4.h:631-643, 726-744): the interval k_runs assumed (the
 // run's first position) may start later, or not at all.  k_prep replays the reference's loop in order

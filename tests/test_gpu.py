@@ -158,9 +158,8 @@ def test_large_roundtrip_property(compressor):
 def test_golden_vectors_on_gpu(compressor, golden):
     for case in golden:
         data = inputs.make(case["input"])
-        if "dict" in case:
-            continue  # dictionary mode: see test_dictionary_mode_unsupported
-        frame = compressor.lz4(data, case["level"], b"", bool(case["legacy"]))
+        dictionary = inputs.make(case["dict"]) if "dict" in case else b""
+        frame = compressor.lz4(data, case["level"], dictionary, bool(case["legacy"]))
         assert inputs.sha(frame) == case["out_sha256"], (case["name"], case["level"], case["legacy"])
 
 
@@ -177,10 +176,18 @@ def test_stream_run_across_block_boundary(compressor):
     assert compressor.lz4(data, 65535) == pyoracle.oz_lz4(data, 65535)
 
 
-def test_dictionary_mode_unsupported(compressor):
-    from smallz4_amd._native import NativeError
-    with pytest.raises(NativeError):
-        compressor.lz4(b"abc" * 1000, 65535, b"dictionary")
+@pytest.mark.parametrize("chain", [3, 6, 9, 65535])
+def test_dictionary_mode(compressor, chain):
+    """Dictionary mode reproduces the reference byte for byte, including its misaligned chain slots
+    (DESIGN.md section 3.7): k_dict_matches replays the match loop, the parse and assembly are shared."""
+    cases = [
+        (synth.enwik8_like(60000, seed=50), synth.enwik8_like(20000, seed=51), False),
+        (synth.enwik8_like(40000, seed=52), synth.enwik8_like(70000, seed=53), False),
+        (bytes(20) + synth.enwik8_like(30000, seed=54), b"short dictionary", False),
+        (synth.enwik8_like(30000, seed=55), synth.enwik8_like(5000, seed=56), True),
+    ]
+    for data, dictionary, legacy in cases:
+        assert compressor.lz4(data, chain, dictionary, legacy) == pyoracle.oz_lz4(data, chain, dictionary, legacy)
 
 
 def test_cpp_dropin_program(tmp_path):
@@ -205,7 +212,9 @@ def test_reference_cli_rebuilt_on_dropin(tmp_path):
     ref = os.path.join(ROOT, "oracle", "_ref", "smallz4")
     src = tmp_path / "in.txt"
     src.write_bytes(synth.enwik8_like(6 << 20, seed=19))
-    for flags in (["-9"], ["-6"], ["-2"], ["-0"], ["-9", "-l"]):
+    dic = tmp_path / "dict.txt"
+    dic.write_bytes(synth.enwik8_like(30000, seed=20))
+    for flags in (["-9"], ["-6"], ["-2"], ["-0"], ["-9", "-l"], ["-D", str(dic), "-9"]):
         a, b = tmp_path / "a.lz4", tmp_path / "b.lz4"
         subprocess.run([amd, "-f", *flags, str(src), str(a)], check=True)
         subprocess.run([ref, "-f", *flags, str(src), str(b)], check=True)
