@@ -33,7 +33,7 @@ from smallz4_amd import synth  # noqa: E402  (input generators; the HIP library 
 
 METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01c_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01d_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
 
 # input shapes (smallz4_amd/synth.py); the default is the headline workload (configs[1])
 DATA = {

@@ -28,7 +28,7 @@ extern "C" {
 #define SZ4_E_DEVICE       -2  /* HIP runtime error                             */
 #define SZ4_E_CAPACITY     -3  /* output buffer too small                       */
 #define SZ4_E_NOMEM        -4  /* device/host allocation failed                 */
-#define SZ4_E_UNSUPPORTED  -5  /* combination not implemented on the device     */
+#define SZ4_E_UNSUPPORTED  -5  /* reserved: every level, format and dictionary is supported */
 
 /* frame header written by sz4_compress_blocks_device */
 #define SZ4_HEADER_SMALLZ4     0  /* exactly smallz4's header: 04 22 4D 18 40 70 DF  */
