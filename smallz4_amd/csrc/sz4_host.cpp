@@ -31,8 +31,6 @@ constexpr uint64_t kSegTargets = 65536;       // target positions per segment
 constexpr uint64_t kBlockMax = 4ull << 20;    // MaxBlockSize (smallz4.h:124)
 constexpr uint64_t kBlockMaxLegacy = 8ull << 20;
 
-uint64_t align_up(uint64_t v, uint64_t a) { return (v + a - 1) / a * a; }
-
 uint64_t token_capacity(uint64_t n) { return n / 2 + 4; }
 
 struct DevBuf {

@@ -1,14 +1,20 @@
 // sz4_kernels.hip -- gfx950 kernels of the LZ4 optimal-parse compressor.
 //
 // Pipeline per batch of blocks (all data resident in HBM):
-//   k_runs      same-letter runs  -> shortcut intervals     (smallz4.h:631-643)
-//   k_sort      per segment: positions sorted by (4-byte key, position); replaces
-//               the previousHash/previousExact chains        (smallz4.h:645-720)
-//   k_find      per position: longest match over the sorted candidate group,
-//               64 candidates per wavefront step             (smallz4.h:173-255)
-//   k_parse     per block, one wavefront: greedy/lazy skip scan, backward
-//               optimal parse, token emission                (smallz4.h:376-472, 259-371, 726-744)
-//   k_scan / k_assemble   block offsets + frame concatenation (smallz4.h:762-813)
+//   k_runs         same-letter runs -> shortcut intervals              (smallz4.h:631-643)
+//   k_sort         per segment: positions sorted by (4-byte key hash, position); replaces the
+//                  previousHash/previousExact chains                   (smallz4.h:645-720)
+//   k_find_sorted  pass 1, lane = target in sorted order: longest match over its key group
+//                                                                      (smallz4.h:173-255)
+//   k_find_long9 / k_find   pass 2 in text order: long matches, big groups, shortcut intervals
+//   k_prep         never-searched positions; greedy/lazy skip replay and shortcut check
+//                                                                      (smallz4.h:726-744)
+//   k_dp_spec / k_dp_fix    backward optimal parse as speculative segments + repair
+//                                                                      (smallz4.h:376-472)
+//   k_walk / k_walk_fix     forward walk of the parse choices          (smallz4.h:259-300)
+//   k_seg_scan, k_seg_tokens, k_block_bytes, k_scan, k_write_seg
+//                  tokens, sizes, stored/compressed decision, frame    (smallz4.h:300-371, 762-813)
+//   k_dict_matches dictionary mode: the reference's match loop replayed by one wavefront
 //
 // Integer/byte work only: no MFMA.  The reference semantics each kernel must
 // reproduce are restated in DESIGN.md section 3.
@@ -106,17 +112,7 @@ constexpr int kRowHalfMirror = 0x141;
 constexpr int kRowMirror = 0x140;
 constexpr int kRowShr = 0x110;        // + n
 constexpr int kWaveShr1 = 0x138;      // wave_shr:1 (whole 64-lane wavefront)
-constexpr int kRowBcast15 = 0x142;    // lane 15 of each row -> the next row (rows in row_mask)
-constexpr int kRowBcast31 = 0x143;    // lane 31 -> rows 2 and 3 (rows in row_mask)
 
-// DPP move restricted to the rows of kRowMask; other rows keep v
-template <int kCtrl>
-__device__ __forceinline__ uint32_t dpp_rows_impl(uint32_t v, int rowMask)
-{
-  return rowMask == 0xA ? (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xA, 0xF, false)
-                        : (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, kCtrl, 0xC, 0xF, false);
-}
-#define dpp_rows(v, ctrl, mask) dpp_rows_impl<ctrl>((v), (mask))
 
 // every lane receives the min / max of its 16-lane row
 __device__ __forceinline__ uint32_t row_min(uint32_t v)
@@ -2746,7 +2742,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
 // Sequences.  The reference walks the parse forward (selectBestMatches, smallz4.h:259-371): a
 // position with a chosen length > 1 starts a match, others are literals.  The walk is split into
 // sub-segments of kWalkSeg positions walked at once (k_walk), repaired where a speculative start
-// was wrong (k_walk_fix), and turned into 16-byte tokens (literal run, match) by k_emit_tokens.
+// was wrong (k_walk_fix), and turned into 16-byte tokens (literal run, match) by k_seg_tokens.
 // ================================================================================================
 
 constexpr int kWalkWaves = 4;  // sub-segments per k_walk workgroup
@@ -2896,77 +2892,8 @@ __device__ __forceinline__ uint64_t token_bytes(uint64_t lits, uint32_t mlen, bo
   return b;
 }
 
-// k_emit_tokens: one 256-thread workgroup per block concatenates its sub-segments' match lists,
-// turns consecutive matches into sequences (literal run before each match, smallz4.h:259-371),
-// sizes the encoding and makes the stored/compressed decision of smallz4.h:764-771.
-__global__ __launch_bounds__(256) void k_emit_tokens(const Block* __restrict__ blocks, uint32_t maxChain,
-                                                     const uint32_t* __restrict__ chosen,
-                                                     const uint16_t* __restrict__ mdist, uint64_t matchBase,
-                                                     const uint32_t* __restrict__ slotsAll,
-                                                     const uint4* __restrict__ state, uint32_t* __restrict__ posAll,
-                                                     Token* __restrict__ tokAll, uint32_t* __restrict__ ntokOut,
-                                                     uint32_t* __restrict__ blockBytes)
-{
-  __shared__ uint64_t s_red[4];
-  __shared__ uint32_t s_pre[4];
-  const Block B = blocks[blockIdx.x];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint64_t n = B.end - B.start;
-  const bool stored = maxChain == 0;
-  const bool legacy = (B.flags & kBlkLegacy) != 0;
-  uint64_t enc = 0;
-  uint32_t ntok = 0;
-  if (!stored) {
-    const uint32_t* L = chosen + (B.start - matchBase);
-    const uint16_t* D = mdist + (B.start - matchBase);
-    uint32_t* posList = posAll + (B.start - matchBase);
-    Token* tok = tokAll + B.tokOff;
-    // 1. concatenate the sub-segments' match positions
-    uint32_t M = 0;
-    for (uint32_t k = 0; k < B.walkCount; k++) {
-      const uint32_t idx = B.walkFirst + k;
-      const uint4 st = state[idx];
-      const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
-      for (uint32_t t = tid; t < st.y - st.x; t += 256) posList[M + t] = slots[st.x + t];
-      M += st.y - st.x;
-    }
-    __syncthreads();
-    // 2. one sequence per match (literals before it), then the closing literal run
-    for (uint32_t t = tid; t <= M; t += 256) {
-      uint32_t prevEnd = 0;
-      if (t > 0) {
-        const uint32_t pp = posList[t - 1];
-        prevEnd = pp + L[pp];
-      }
-      if (t < M) {
-        const uint32_t p = posList[t], lits = p - prevEnd, Lm = L[p];
-        tok[t] = Token{lits ? prevEnd : 0u, lits, Lm, (uint32_t)D[p]};
-        enc += token_bytes(lits, Lm, false);
-      } else {
-        tok[t] = Token{prevEnd, (uint32_t)(n - prevEnd), 0u, kTokLast};
-        enc += token_bytes(n - prevEnd, 0, true);
-      }
-    }
-    // workgroup sum of the encoded size
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) enc += __shfl_xor(enc, d, 64);
-    if (lane == 0) s_red[wave] = enc;
-    __syncthreads();
-    enc = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-    ntok = M + 1;
-  }
-  (void)s_pre;
-  const bool useEnc = (enc < n && !stored) || legacy;
-  const uint32_t bytes = (uint32_t)(useEnc ? enc : n);
-  if (tid == 0) {
-    ntokOut[blockIdx.x] = useEnc ? ntok : 0u;
-    blockBytes[blockIdx.x] = (useEnc ? 0u : 0x80000000u) | (bytes + 4u);
-  }
-}
-
 // ================================================================================================
-// k_scan + k_assemble: frame = header, then each block's word + payload (or its raw bytes when
-// the block is stored), then the end mark.
+// k_scan: block offsets in the frame (header, then each block's word + payload, then the end mark)
 // ================================================================================================
 __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ blockBytes, uint32_t nblocks,
                                                uint64_t* __restrict__ offsets)
@@ -2994,69 +2921,226 @@ __global__ __launch_bounds__(1024) void k_scan(const uint32_t* __restrict__ bloc
 
 constexpr uint64_t kOwnLits = 64;  // longer literal runs are copied by the whole workgroup
 
-// k_write: one 256-thread workgroup per block writes the block word and either the raw bytes
-// (stored block) or its tokens: token offsets by a workgroup scan of token sizes, then every
-// thread encodes one token (smallz4.h:310-367) straight into the frame.
-__global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
-                                               const Token* __restrict__ tokAll, const uint32_t* __restrict__ ntokAll,
-                                               const uint32_t* __restrict__ blockBytes, const uint64_t* __restrict__ offsets,
-                                               uint8_t* __restrict__ out, uint64_t headerLen)
+// ================================================================================================
+// Frame assembly by walk sub-segment (kWalkSeg positions), so that large blocks fill the GPU too:
+//   k_seg_scan    per block: exclusive scans over its sub-segments of the match counts (token base)
+//                 and of the match ends (the end of the last match before the sub-segment)
+//   k_seg_tokens  per sub-segment: its tokens (literal run + match, smallz4.h:259-371), their byte
+//                 sizes summed; the block's last sub-segment adds the closing literal run
+//   k_block_bytes per block: byte offsets of the sub-segments, encoded size, stored/compressed
+//                 decision (smallz4.h:764-771)
+//   k_scan        block offsets in the frame
+//   k_write_seg   per sub-segment: its tokens (or its raw bytes) at their place in the frame
+// ================================================================================================
+constexpr int kAsmThreads = 1024;
+constexpr int kSegWaves = 4;  // sub-segments per k_seg_tokens / k_write_seg workgroup
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v)
 {
-  __shared__ uint64_t s_w[4];
-  __shared__ uint64_t s_carry;
-  __shared__ uint32_t s_nLong;
-  __shared__ uint32_t s_longDst[256], s_longSrc[256], s_longLen[256];  // long literal runs of one round
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+  return v;
+}
+
+// info[idx] = (token base, end of the last match before, byte size, byte offset) per sub-segment
+__global__ __launch_bounds__(kAsmThreads) void k_seg_scan(const Block* __restrict__ blocks, const uint32_t* __restrict__ chosen,
+                                                          uint64_t matchBase, const uint32_t* __restrict__ slotsAll,
+                                                          const uint4* __restrict__ state, uint4* __restrict__ info)
+{
+  __shared__ uint32_t s_sum[kAsmThreads / 64], s_max[kAsmThreads / 64];
+  const Block B = blocks[blockIdx.x];
+  const uint32_t* L = chosen + (B.start - matchBase);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t carrySum = 0, carryMax = 0;
+  for (uint32_t k0 = 0; k0 < B.walkCount; k0 += kAsmThreads) {
+    const uint32_t k = k0 + tid;
+    const bool valid = k < B.walkCount;
+    const uint32_t idx = B.walkFirst + k;
+    uint32_t cnt = 0, lastEnd = 0;
+    if (valid) {
+      const uint4 st = state[idx];
+      cnt = st.y - st.x;
+      if (cnt) {
+        const uint32_t p = slotsAll[(uint64_t)idx * (2 * kWalkCap) + st.y - 1];
+        lastEnd = p + L[p];
+      }
+    }
+    const uint32_t incS = wave_incl_scan_add(cnt), incM = wave_incl_scan_max(lastEnd);
+    uint32_t prevM = __shfl_up(incM, 1, 64);
+    if (lane == 0) prevM = 0;
+    if (lane == 63) {
+      s_sum[wave] = incS;
+      s_max[wave] = incM;
+    }
+    __syncthreads();
+    uint32_t preS = carrySum, preM = carryMax;
+    for (uint32_t w = 0; w < wave; w++) {
+      preS += s_sum[w];
+      preM = s_max[w] > preM ? s_max[w] : preM;
+    }
+    if (valid) info[idx] = make_uint4(preS + incS - cnt, prevM > preM ? prevM : preM, 0u, 0u);
+    for (uint32_t w = 0; w < kAsmThreads / 64; w++) {
+      carrySum += s_sum[w];
+      carryMax = s_max[w] > carryMax ? s_max[w] : carryMax;
+    }
+    __syncthreads();
+  }
+}
+
+// tokens of one sub-segment; blockTail[b] = (matches of the block, bytes of its closing literal run)
+__global__ __launch_bounds__(64 * kSegWaves) void k_seg_tokens(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
+                                                              uint32_t nwalk, const uint32_t* __restrict__ chosen,
+                                                              const uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                                              const uint32_t* __restrict__ slotsAll, const uint4* __restrict__ state,
+                                                              uint4* __restrict__ info, Token* __restrict__ tokAll,
+                                                              uint2* __restrict__ blockTail)
+{
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kSegWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  const uint32_t* L = chosen + (B.start - matchBase);
+  const uint16_t* D = mdist + (B.start - matchBase);
+  const uint4 st = state[idx];
+  const uint4 inf = info[idx];
+  const uint32_t m = st.y - st.x;
+  const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+  Token* tok = tokAll + B.tokOff + inf.x;
+  uint32_t carryEnd = inf.y, bytes = 0;
+  for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+    const uint32_t t = c0 + lane;
+    const bool valid = t < m;
+    const uint32_t p = valid ? slots[st.x + t] : 0u;
+    const uint32_t Lm = valid ? L[p] : 0u;
+    const uint32_t end = p + Lm;
+    uint32_t prev = __shfl_up(end, 1, 64);
+    if (lane == 0) prev = carryEnd;
+    uint32_t sz = 0;
+    if (valid) {
+      const uint32_t lits = p - prev;
+      tok[t] = Token{lits ? prev : 0u, lits, Lm, (uint32_t)D[p]};
+      sz = (uint32_t)token_bytes(lits, Lm, false);
+    }
+    bytes += wave_sum_u32(sz);
+    carryEnd = rdlane(end, m - c0 < 64 ? m - c0 - 1 : 63);
+  }
+  if (lane == 0) info[idx].z = bytes;
+  if (ws.y + 1 == B.walkCount && lane == 0) {
+    // the closing literal run (kTokLast)
+    const uint32_t M = inf.x + m;
+    tokAll[B.tokOff + M] = Token{carryEnd, n - carryEnd, 0u, kTokLast};
+    blockTail[ws.x] = make_uint2(M, (uint32_t)token_bytes(n - carryEnd, 0, true));
+  }
+}
+
+// per block: byte offsets of its sub-segments, its encoded size and the stored/compressed decision
+__global__ __launch_bounds__(kAsmThreads) void k_block_bytes(const Block* __restrict__ blocks, uint32_t maxChain,
+                                                             uint4* __restrict__ info, const uint2* __restrict__ blockTail,
+                                                             uint32_t* __restrict__ ntokOut, uint32_t* __restrict__ blockBytes)
+{
+  __shared__ uint32_t s_sum[kAsmThreads / 64];
   const Block B = blocks[blockIdx.x];
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const uint32_t bb = blockBytes[blockIdx.x];
-  const bool raw = (bb & 0x80000000u) != 0;
-  const uint32_t bytes = (bb & 0x7FFFFFFFu) - 4u;
-  uint8_t* dst = out + headerLen + offsets[blockIdx.x];
+  const uint64_t n = B.end - B.start;
+  const bool stored = maxChain == 0;
+  const bool legacy = (B.flags & kBlkLegacy) != 0;
+  uint64_t enc = 0;
+  uint32_t ntok = 0;
+  if (!stored) {
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < B.walkCount; k0 += kAsmThreads) {
+      const uint32_t k = k0 + tid;
+      const bool valid = k < B.walkCount;
+      const uint32_t idx = B.walkFirst + k;
+      const uint32_t b = valid ? info[idx].z : 0u;
+      const uint32_t inc = wave_incl_scan_add(b);
+      if (lane == 63) s_sum[wave] = inc;
+      __syncthreads();
+      uint32_t pre = carry;
+      for (uint32_t w = 0; w < wave; w++) pre += s_sum[w];
+      if (valid) info[idx].w = pre + inc - b;
+      for (uint32_t w = 0; w < kAsmThreads / 64; w++) carry += s_sum[w];
+      __syncthreads();
+    }
+    const uint2 tail = blockTail[blockIdx.x];
+    enc = (uint64_t)carry + tail.y;
+    ntok = tail.x + 1;
+  }
+  const bool useEnc = (enc < n && !stored) || legacy;
+  const uint32_t bytes = (uint32_t)(useEnc ? enc : n);
   if (tid == 0) {
-    const uint32_t word = bytes | (raw ? 0x80000000u : 0u);
+    ntokOut[blockIdx.x] = useEnc ? ntok : 0u;
+    blockBytes[blockIdx.x] = (useEnc ? 0u : 0x80000000u) | (bytes + 4u);
+  }
+}
+
+// one wavefront per sub-segment writes its tokens (or its raw bytes) into the frame
+__global__ __launch_bounds__(64 * kSegWaves) void k_write_seg(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                                             const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                             const uint4* __restrict__ state, const uint4* __restrict__ info,
+                                                             const Token* __restrict__ tokAll, const uint32_t* __restrict__ ntokAll,
+                                                             const uint32_t* __restrict__ blockBytes,
+                                                             const uint64_t* __restrict__ offsets, uint8_t* __restrict__ out,
+                                                             uint64_t headerLen)
+{
+  __shared__ uint32_t s_ld[kSegWaves][64], s_ls[kSegWaves][64], s_ll[kSegWaves][64];  // long literal runs
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kSegWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const Block B = blocks[ws.x];
+  const uint64_t n = B.end - B.start;
+  const uint32_t bb = blockBytes[ws.x];
+  const bool raw = (bb & 0x80000000u) != 0;
+  uint8_t* dst = out + headerLen + offsets[ws.x];
+  if (ws.y == 0 && lane == 0) {
+    const uint32_t word = ((bb & 0x7FFFFFFFu) - 4u) | (raw ? 0x80000000u : 0u);
     dst[0] = (uint8_t)word;
     dst[1] = (uint8_t)(word >> 8);
     dst[2] = (uint8_t)(word >> 16);
     dst[3] = (uint8_t)(word >> 24);
-    s_carry = 0;
   }
   dst += 4;
   const uint8_t* src = in + B.start;
   if (raw) {
-    for (uint64_t k = tid; k < bytes; k += 256) dst[k] = src[k];
+    const uint64_t lo = (uint64_t)ws.y * kWalkSeg, hi = lo + kWalkSeg < n ? lo + kWalkSeg : n;
+    for (uint64_t j = lo + lane; j < hi; j += 64) dst[j] = src[j];
     return;
   }
-  const Token* tok = tokAll + B.tokOff;
-  const uint32_t ntok = ntokAll[blockIdx.x];
-  __syncthreads();
-  for (uint32_t base = 0; base < ntok; base += 256) {
-    if (tid == 0) s_nLong = 0;
-    const uint32_t t = base + tid;
+  if (ntokAll[ws.x] == 0) return;  // legacy frame at level 0: an empty compressed block
+  const uint4 st = state[idx], inf = info[idx];
+  const uint32_t count = (st.y - st.x) + (ws.y + 1 == B.walkCount ? 1u : 0u);
+  const Token* tok = tokAll + B.tokOff + inf.x;
+  uint64_t carry = inf.w;
+  for (uint32_t c0 = 0; c0 < count; c0 += 64) {
+    const uint32_t t = c0 + lane;
+    const bool valid = t < count;
     Token T{0, 0, 0, 0};
     uint64_t sz = 0;
-    const bool last = t < ntok && (tok[t].dist & kTokLast);
-    if (t < ntok) {
+    bool last = false;
+    if (valid) {
       T = tok[t];
+      last = (T.dist & kTokLast) != 0;
       sz = token_bytes(T.lits, T.mlen, last);
     }
-    // workgroup exclusive scan of token sizes
     uint64_t incl = sz;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
       const uint64_t o = __shfl_up(incl, d, 64);
       if (lane >= (uint32_t)d) incl += o;
     }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint64_t off = s_carry + incl - sz;
-    for (uint32_t w = 0; w < wave; w++) off += s_w[w];
-    __syncthreads();
-    if (tid == 255) s_carry = off + sz;
-    if (t < ntok) {
+    const uint64_t off = carry + incl - sz;
+    carry += __shfl(incl, 63, 64);
+    bool isLong = false;
+    if (valid) {
       uint8_t* o = dst + off;
       const int64_t mcode = last ? 0 : (int64_t)T.mlen - kMinMatch;
       const uint8_t tk = (uint8_t)(mcode < 15 ? mcode : 15);
-      uint64_t lits = T.lits;
+      const uint64_t lits = T.lits;
       if (lits < 15) {
         *o++ = (uint8_t)(tk | (lits << 4));
       } else {
@@ -3065,15 +3149,13 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
         while (v >= 255) { *o++ = 255; v -= 255; }
         *o++ = (uint8_t)v;
       }
-      const uint8_t* ls = src + T.litFrom;
       if (lits <= kOwnLits) {
-        for (uint64_t k = 0; k < lits; k++) o[k] = ls[k];
+        for (uint64_t k = 0; k < lits; k++) o[k] = src[T.litFrom + k];
       } else {
-        // copied by the whole workgroup below
-        const uint32_t slot = atomicAdd(&s_nLong, 1u);
-        s_longDst[slot] = (uint32_t)(o - dst);
-        s_longSrc[slot] = T.litFrom;
-        s_longLen[slot] = (uint32_t)lits;
+        isLong = true;  // copied by the whole wavefront below
+        s_ld[wave][lane] = (uint32_t)(o - dst);
+        s_ls[wave][lane] = T.litFrom;
+        s_ll[wave][lane] = (uint32_t)lits;
       }
       o += lits;
       if (!last) {
@@ -3088,13 +3170,15 @@ __global__ __launch_bounds__(256) void k_write(const uint8_t* __restrict__ in, c
         }
       }
     }
-    __syncthreads();
-    for (uint32_t r = 0; r < s_nLong; r++) {
-      uint8_t* d = dst + s_longDst[r];
-      const uint8_t* ls = src + s_longSrc[r];
-      for (uint32_t k = tid; k < s_longLen[r]; k += 256) d[k] = ls[k];
+    uint64_t longs = __ballot(isLong);
+    while (longs) {
+      const uint32_t l = (uint32_t)__builtin_ctzll(longs);
+      longs &= longs - 1;
+      uint8_t* d = dst + s_ld[wave][l];
+      const uint8_t* ls = src + s_ls[wave][l];
+      const uint32_t len = s_ll[wave][l];
+      for (uint32_t k = lane; k < len; k += 64) d[k] = ls[k];
     }
-    __syncthreads();
   }
 }
 
@@ -3200,10 +3284,20 @@ void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
                        nwalk, chosen, matchBase, walkSlots, walkState);
     hipLaunchKernelGGL(k_walk_fix, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState);
   }
-  hipLaunchKernelGGL(k_emit_tokens, dim3(nblocks), dim3(256), 0, s, blocks, maxChain, chosen, mdist, matchBase, walkSlots,
-                     walkState, posList, tokens, ntok, blockBytes);
+  // per-sub-segment scratch in posList (the parse's reach array, free by now)
+  uint4* info = reinterpret_cast<uint4*>(posList);
+  uint2* blockTail = reinterpret_cast<uint2*>(info + nwalk);
+  const uint32_t segGrid = (nwalk + kSegWaves - 1) / kSegWaves;
+  if (maxChain > 0 && nwalk) {
+    hipLaunchKernelGGL(k_seg_scan, dim3(nblocks), dim3(kAsmThreads), 0, s, blocks, chosen, matchBase, walkSlots, walkState, info);
+    hipLaunchKernelGGL(k_seg_tokens, dim3(segGrid), dim3(64 * kSegWaves), 0, s, blocks, walkSegs, nwalk, chosen, mdist, matchBase,
+                       walkSlots, walkState, info, tokens, blockTail);
+  }
+  hipLaunchKernelGGL(k_block_bytes, dim3(nblocks), dim3(kAsmThreads), 0, s, blocks, maxChain, info, blockTail, ntok, blockBytes);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, blockBytes, nblocks, offsets);
-  hipLaunchKernelGGL(k_write, dim3(nblocks), dim3(256), 0, s, in, blocks, tokens, ntok, blockBytes, offsets, out, headerLen);
+  if (nwalk)
+    hipLaunchKernelGGL(k_write_seg, dim3(segGrid), dim3(64 * kSegWaves), 0, s, in, blocks, walkSegs, nwalk, walkState, info, tokens,
+                       ntok, blockBytes, offsets, out, headerLen);
 }
 
 }  // namespace sz4
