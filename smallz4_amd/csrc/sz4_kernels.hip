@@ -1479,25 +1479,104 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
 
   // a stretch from q: best matches one after the other, each carrying into the next; ends at the
   // piece boundary or the first target pass 1 finished
+  // one target per lane (a speculative batch): the same result as best_of under the same carry,
+  // each lane walking its own candidates (class runs jumped with skip pointers)
+  auto best_lane = [&](uint64_t p, uint32_t cLen, uint32_t cDist, uint32_t& bLen, uint32_t& bDist) {
+    const uint32_t key = src.ld4(p);
+    const uint32_t room = (uint32_t)(stopAbs - p);
+    const uint64_t lb = p > kWindow ? p - kWindow : 0;  // no lookback cut on this path
+    uint32_t bestLen = 0, bestDist = 0;
+    bool carryOk = false;
+    if (cDist != 0u && cLen >= 5u) {
+      const uint64_t c = p - cDist;
+      if (c >= lb && !excluded(c)) {
+        bestLen = cLen - 1;
+        bestDist = cDist;
+        carryOk = true;
+      }
+    }
+    if (!(carryOk && bestLen >= room && bestDist == 1u)) {
+      const bool prune = carryOk || cLen < 5u;
+      const uint32_t pc = prune ? (src.ld4(p - 1) & 0xFFu) : 0xFFFFu;
+      const uint32_t slot = rank[p - S.s0];
+      const int32_t gs = (int32_t)slot_gs(compact, small, E, slot);
+      int32_t sl = (int32_t)slot - 1;
+      while (sl >= gs) {
+        const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)sl);
+        if (c < lb) break;  // positions descend: everything farther is out of the window
+        if (prune && pred_class(c) == pc) {
+          sl = skip[sl];  // a run of pruned candidates
+          continue;
+        }
+        const uint32_t dist = (uint32_t)(p - c);
+        if (bestDist != 0u && bestLen >= room && dist >= bestDist) break;  // only nearer ties could win
+        if (src.ld4(c) == key) {
+          const uint32_t need = bestDist == 0u ? 4u : (dist < bestDist ? bestLen : bestLen + 1u);
+          const uint32_t got = prefix_if_at_least(src, p, c, need < 4u ? 4u : need, room);
+          if (got >= need && got != 0u && (got > bestLen || dist < bestDist)) {
+            bestLen = got;
+            bestDist = dist;
+          }
+        }
+        sl--;
+      }
+    }
+    bLen = bestDist ? bestLen : 0u;
+    bDist = bestDist;
+  };
+
+  // a stretch from q: best matches in order, each carrying into the next; ends at the piece boundary
+  // or the first target pass 1 finished.  With an exact carry (cLen, cDist) the next targets are
+  // taken 64 at a time, one per lane, on the hypothesis that the carried match goes on: lane t
+  // assumes best(q + t - 1) = (cLen - t, cDist).  Lane 0's carry is exact, and the first lane whose
+  // result breaks the chain is exact too (its predecessor kept the hypothesis); the batch is taken up
+  // to that lane and the next one starts after it with its result as the carry.
   auto walk_stretch = [&](uint64_t q, uint32_t cLen, uint32_t cDist, bool exact) {
     bool rmqLen = false;
-    uint32_t bits = longBits[(q - matchBase) >> 5];  // this stretch's long bits, a word at a time
-    while (true) {
+    // stretch end: piece boundary, segment end or first unmarked target
+    const uint64_t pieceEnd = S.s0 + (((q - S.s0) / kPiece) + 1) * kPiece;
+    const uint64_t lim = pieceEnd < S.s1 ? pieceEnd : S.s1;
+    uint64_t qEnd = q;
+    while (qEnd < lim) {
+      const uint64_t qi = qEnd - matchBase;
+      const uint32_t w = longBits[qi >> 5] >> (qi & 31);  // the word's bits from qEnd on
+      const uint32_t ones = (uint32_t)__builtin_ctzll(~(uint64_t)w);  // <= 32 - (qi & 31)
+      qEnd += ones;
+      if (ones < 32u - (uint32_t)(qi & 31)) break;
+    }
+    if (qEnd > lim) qEnd = lim;
+    while (q < qEnd) {
       uint32_t bLen, bDist;
-      best_of(q, cLen, cDist, exact, bLen, bDist);
-      if (lane == 0) {
-        mlen[q - matchBase] = bLen;
-        mdist[q - matchBase] = (uint16_t)bDist;
+      const uint64_t left = qEnd - q;
+      const uint32_t spec = exact && cut == kNone && cDist != 0u && cLen >= 6u
+                                ? (uint32_t)min<uint64_t>(min<uint64_t>(64, left), cLen - 5u) : 0u;
+      if (spec >= 2) {
+        const bool mine = lane < spec;
+        uint32_t rL = 0, rD = 0;
+        if (mine) best_lane(q + lane, cLen - lane, cDist, rL, rD);
+        const bool keeps = rL == cLen - 1u - lane && rD == cDist;
+        const uint64_t breaks = __ballot(mine && !keeps);
+        const uint32_t f = breaks ? (uint32_t)__builtin_ctzll(breaks) : spec - 1u;  // last lane taken
+        if (lane <= f) {
+          mlen[q + lane - matchBase] = rL;
+          mdist[q + lane - matchBase] = (uint16_t)rD;
+        }
+        rmqLen |= __ballot(lane <= f && rL >= kRmqLen && !(rD == 1u && rL >= kSameLetter)) != 0;
+        bLen = rdlane(rL, f);
+        bDist = rdlane(rD, f);
+        q += f + 1;
+      } else {
+        best_of(q, cLen, cDist, exact, bLen, bDist);
+        if (lane == 0) {
+          mlen[q - matchBase] = bLen;
+          mdist[q - matchBase] = (uint16_t)bDist;
+        }
+        rmqLen |= bLen >= kRmqLen && !(bDist == 1u && bLen >= kSameLetter);
+        q++;
       }
-      rmqLen |= bLen >= kRmqLen && !(bDist == 1u && bLen >= kSameLetter);
       cLen = bLen;
       cDist = bDist;
       exact = true;
-      q++;
-      if (q >= S.s1 || ((q - S.s0) & (kPiece - 1)) == 0) break;
-      const uint64_t qi = q - matchBase;
-      if ((qi & 31) == 0) bits = longBits[qi >> 5];
-      if (!((bits >> (qi & 31)) & 1u)) break;
     }
     if (rmqLen && lane == 0) atomicOr(&longFlag[S.block], 1u);
   };
