@@ -675,14 +675,18 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
     s_next = 0;
     s_long = 0;
   }
-  Bytes<kLds> src;
-  if constexpr (kLds) {
-    const uint32_t words = (uint32_t)((B.end - S.w0 + 8 + 3) / 4);
+  // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM
+  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
+  {
+    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
+    const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
     for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
     src.w = win;
     src.base = S.w0;
-  } else {
-    src.in = in;
+    if constexpr (!kLds) {
+      src.lim = S.w0 + 4ull * words;
+      src.in = in;
+    }
   }
   __syncthreads();
 
@@ -2624,11 +2628,29 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     uint32_t closedCost = 0;  // closed-form chunk: cost at its end closedE
     int32_t closedE = 0;
     bool done = false;
+    // the chunk's inputs are loaded one chunk ahead (positions below are not rewritten before)
+    uint32_t nL, nD, nS, nC, nR;
+    auto load_chunk = [&](int32_t h) {
+      const int32_t ip = h - (int32_t)lane;
+      const bool in = ip >= lo;
+      nL = in ? L[ip] : 0u;
+      nD = in ? (uint32_t)D[ip] : 0u;
+      nS = in ? S[ip] : 0u;
+      nC = in ? cost[ip] : 0u;
+      nR = in ? R[ip] : 0u;
+    };
+    load_chunk(hi);
     for (int32_t h = hi; h >= lo && !done; h -= 64) {
       const int32_t ip = h - (int32_t)lane;
       const bool in = ip >= lo;
-      const uint32_t cL = in ? L[ip] : 0u, cD = in ? (uint32_t)D[ip] : 0u;
-      const uint32_t cS = in ? S[ip] : 0u, cC = in ? cost[ip] : 0u, cR = in ? R[ip] : 0u;
+      uint32_t cL, cD, cS, cC, cR;
+      // opaque copies: the loop below must not wait for the prefetch issued right after
+      asm volatile("v_mov_b32 %0, %1" : "=v"(cL) : "v"(nL));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(cD) : "v"(nD));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(cS) : "v"(nS));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(cC) : "v"(nC));
+      asm volatile("v_mov_b32 %0, %1" : "=v"(cR) : "v"(nR));
+      if (h - 64 >= lo) load_chunk(h - 64);
       const int32_t cl = h - 63 > lo ? h - 63 : lo;
       const uint32_t cnt = (uint32_t)(h - cl + 1);
       if (__ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
@@ -3307,9 +3329,15 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
                          compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
   } else {
-    if (pass == 1)
-      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact,
-                         maxChain, mlen, mdist, matchBase, longBits, segLong);
+    if (pass == 1) {
+      static uint32_t attrBytes1 = 0;
+      if (hybridLds > attrBytes1) {
+        hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+        attrBytes1 = hybridLds;
+      }
+      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+                         compact, maxChain, mlen, mdist, matchBase, longBits, segLong);
+    }
     else if (unlimited) {
       static uint32_t attrBytes = 0;
       if (hybridLds > attrBytes) {
