@@ -57,6 +57,7 @@ def parse_args():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
     ap.add_argument("--verify-threads", type=int, default=16)
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-decode", action="store_true", help="skip the decoder leg (sz4_unlz4_device)")
     ap.add_argument("--data", default="enwik8", choices=sorted(DATA),
                     help="synthetic input shape (enwik8: configs[1]; zeros_urandom: configs[4])")
     return ap.parse_args()
@@ -163,6 +164,24 @@ def main():
     stages = {k: v / args.steps for k, v in stage_sum.items()}
     frame = out[:size].cpu().numpy().tobytes()
 
+    # decoder leg (smallz4cat semantics on the device, sz4_unlz4_device), outside the timed region:
+    # the frame just written, decoded back into HBM and compared with the input
+    dec = None
+    if not args.no_decode:
+        dout = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
+        comp.unlz4_device(out.data_ptr(), size, dout.data_ptr(), nbytes, stream=stream)
+        torch.cuda.synchronize(local)
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            got = comp.unlz4_device(out.data_ptr(), size, dout.data_ptr(), nbytes, stream=stream)
+        torch.cuda.synchronize(local)
+        dt = (time.perf_counter() - t0) / reps
+        dec = {"value": round(nbytes / dt / 1e6, 1), "unit": "MB/s of decoded output (host-timed call: index, "
+               "sizes and decode launches with their syncs)", "ms": round(dt * 1e3, 3),
+               "roundtrip_equal": bool(got == nbytes and torch.equal(dout, t_in))}
+        del dout
+
     # output-byte diff against the reference, every block of every rank
     diff, verified, kind = -1, 0, None
     if not args.no_verify:
@@ -214,6 +233,8 @@ def main():
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes},
         }
+        if dec is not None:
+            rec["unlz4"] = dec
         if world == 1:
             rec["cpu_baseline"] = cpu_baseline(data, args.block_size, chain, args.cpu_seconds)
         print(json.dumps(rec), flush=True)

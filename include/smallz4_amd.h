@@ -29,6 +29,7 @@ extern "C" {
 #define SZ4_E_CAPACITY     -3  /* output buffer too small                       */
 #define SZ4_E_NOMEM        -4  /* device/host allocation failed                 */
 #define SZ4_E_UNSUPPORTED  -5  /* reserved: every level, format and dictionary is supported */
+#define SZ4_E_CORRUPT      -6  /* decoder: a frame the reference decoder rejects           */
 
 /* frame header written by sz4_compress_blocks_device */
 #define SZ4_HEADER_SMALLZ4     0  /* exactly smallz4's header: 04 22 4D 18 40 70 DF  */
@@ -98,6 +99,25 @@ void sz4_set_timing(sz4_ctx* ctx, int on);
  * are the parse's choices (1 = literal).  Used by the intermediate parity tests. */
 void sz4_debug_stop_after(sz4_ctx* ctx, int stop_after);
 int sz4_debug_matches(sz4_ctx* ctx, uint32_t* len, uint16_t* dist, uint64_t n);
+
+/* ---- decoder: the reference's smallz4cat ------------------------------------------------------
+ * Decompress an LZ4 frame with the semantics of the reference decoder
+ *   unlz4_userPtr(GET_BYTE, SEND_BYTES, dictionary, userPtr)      smallz4cat.c:112-360
+ * over memory: modern and legacy frames, stored blocks, skipped block / content checksums,
+ * content size and dictionary ID, an optional dictionary (its last 64 KiB precede the output),
+ * a legacy frame ending after its first block shorter than 8 MiB.  Every byte is decoded on the
+ * GPU (one wavefront per block).
+ *   out_size  receives the decoded size, also when out_cap is too small (SZ4_E_CAPACITY):
+ *             call with out = NULL, out_cap = 0 to query it
+ * Returns SZ4_E_CORRUPT for a frame the reference decoder rejects (signature, version, truncated
+ * frame, offset 0) or would misread (a length, literal run or offset crossing its block). */
+int sz4_unlz4(sz4_ctx* ctx, const void* frame, uint64_t frame_len, const void* dict, uint64_t dict_len,
+              void* out, uint64_t out_cap, uint64_t* out_size);
+
+/* The same on device memory (frame, dictionary and output are device pointers) and a HIP stream;
+ * returns after the stream has finished. */
+int sz4_unlz4_device(sz4_ctx* ctx, const void* d_frame, uint64_t frame_len, const void* d_dict,
+                     uint64_t dict_len, void* d_out, uint64_t out_cap, uint64_t* out_size, void* stream);
 
 /* Last error message of the context ("" if none). */
 const char* sz4_last_error(sz4_ctx* ctx);

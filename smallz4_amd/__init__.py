@@ -116,6 +116,31 @@ class Compressor:
                                            block_size, max_chain_length, header, stream)
         return out[:size].cpu().numpy().tobytes()
 
+    # -- decoder: the reference's smallz4cat -----------------------------------------------------
+    def unlz4(self, frame: bytes, dictionary: bytes = b"") -> bytes:
+        """smallz4cat's unlz4 (smallz4cat.c:112-360) on the GPU: the bytes `frame` decodes to.
+        Raises NativeError for a frame the reference decoder rejects."""
+        frame, dic = bytes(frame), bytes(dictionary)
+        size = ctypes.c_uint64()
+        rc = self._lib.sz4_unlz4(self._h, frame, len(frame), dic or None, len(dic), None, 0, ctypes.byref(size))
+        if rc == _native.SZ4_OK:
+            return b""
+        if rc != _native.SZ4_E_CAPACITY:
+            self._check(rc, "sz4_unlz4")
+        out = ctypes.create_string_buffer(size.value)
+        rc = self._lib.sz4_unlz4(self._h, frame, len(frame), dic or None, len(dic), out, size.value, ctypes.byref(size))
+        self._check(rc, "sz4_unlz4")
+        return out.raw[:size.value]
+
+    def unlz4_device(self, d_frame: int, n: int, d_out: int, out_cap: int, d_dict: int = 0, dict_len: int = 0,
+                     stream: int = 0) -> int:
+        """Device pointers in, decoded size out (see sz4_unlz4_device); raises when out_cap is too small."""
+        size = ctypes.c_uint64()
+        rc = self._lib.sz4_unlz4_device(self._h, ctypes.c_void_p(d_frame), n, ctypes.c_void_p(d_dict), dict_len,
+                                        ctypes.c_void_p(d_out), out_cap, ctypes.byref(size), ctypes.c_void_p(stream))
+        self._check(rc, "sz4_unlz4_device")
+        return size.value
+
     def last_block_sizes(self, nblocks: int) -> list[int]:
         arr = (ctypes.c_uint32 * max(nblocks, 1))()
         k = self._lib.sz4_last_block_sizes(self._h, arr, nblocks)
@@ -161,3 +186,8 @@ def lz4(data: bytes, max_chain_length: int = MaxChainLength, dictionary: bytes =
 def compress_blocks(data, block_size: int = 65536, max_chain_length: int = MaxChainLength,
                     header: str = "smallz4") -> bytes:
     return _ctx().compress_blocks(data, block_size, max_chain_length, header)
+
+
+def unlz4(frame: bytes, dictionary: bytes = b"") -> bytes:
+    """smallz4cat's decoder (smallz4cat.c:112-360) on the GPU."""
+    return _ctx().unlz4(frame, dictionary)

@@ -13,6 +13,8 @@ LIB_PATH = os.environ.get("SMALLZ4_AMD_LIB") or os.path.join(os.path.dirname(os.
                                                                "libsmallz4_amd.so")
 
 SZ4_OK = 0
+SZ4_E_CAPACITY = -3
+SZ4_E_CORRUPT = -6
 SZ4_HEADER_SMALLZ4 = 0
 SZ4_HEADER_INDEPENDENT = 1
 SZ4_HEADER_NONE = 2
@@ -32,6 +34,8 @@ SIGNATURES = {
     "sz4_set_timing": (None, [_vp, _i32]),
     "sz4_debug_stop_after": (None, [_vp, _i32]),
     "sz4_debug_matches": (_i32, [_vp, _vp, _vp, _u64]),
+    "sz4_unlz4": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
+    "sz4_unlz4_device": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     "sz4_last_error": (ctypes.c_char_p, [_vp]),
 }
 

@@ -88,6 +88,8 @@ struct sz4_ctx {
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
   DevBuf dictLast, dictPrevH;  // dictionary mode: the reference's hash table and hash chain
+  DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut;  // decoder (sz4_unlz4*)
+  std::vector<UnBlock> hUn;
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
 
@@ -325,6 +327,72 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   return SZ4_OK;
 }
 
+// ---- decoder (the reference's smallz4cat) ----------------------------------------------------
+// Index and sizes passes: every block's output offset.  A legacy frame ends after its first block
+// shorter than 8 MiB (smallz4cat.c:325-327), so a malformed tail after that block does not matter.
+// *keep = blocks to decode, *total = decoded bytes.
+int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32_t* keep, hipStream_t s)
+{
+  hipError_t e;
+  uint64_t maxBlocks = std::min<uint64_t>(n / 5 + 2, 1u << 16);  // a block takes >= 5 frame bytes
+  uint64_t meta[3] = {0, 0, 0};
+  for (;;) {
+    if ((e = c->unBlk.reserve(maxBlocks * sizeof(UnBlock) + 64)) || (e = c->unMeta.reserve(64)))
+      return c->fail(SZ4_E_NOMEM, "decoder scratch", e);
+    launch_unlz4_index(f, n, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
+    if ((e = hipMemcpyAsync(meta, c->unMeta.p, sizeof meta, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "frame index", e);
+    if (meta[1] != 2) break;
+    maxBlocks = n / 5 + 2;
+  }
+  const uint32_t nb = (uint32_t)meta[0];
+  c->hUn.resize(nb);
+  if (nb) {
+    launch_unlz4_sizes(f, n, c->unBlk.as<UnBlock>(), nb, s);
+    if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "block sizes", e);
+  }
+  uint64_t w = 0;
+  uint32_t k = 0;
+  bool ended = false;
+  while (k < nb) {
+    UnBlock& b = c->hUn[k++];
+    if (b.size == kNone) return c->fail(SZ4_E_CORRUPT, "malformed LZ4 block");
+    b.dst = w;
+    w += b.size;
+    if (meta[2] && b.size < kBlockMaxLegacy) {
+      ended = true;
+      break;
+    }
+  }
+  if (meta[1] != 0 && !ended) return c->fail(SZ4_E_CORRUPT, "invalid or truncated LZ4 frame");
+  *total = w;
+  *keep = k;
+  return SZ4_OK;
+}
+
+int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, uint64_t dl, uint8_t* out, uint32_t keep,
+                 hipStream_t s)
+{
+  if (!keep) return SZ4_OK;
+  hipError_t e;
+  const uint64_t flagBytes = ((uint64_t)keep + 2) * 4;
+  if ((e = c->unFlags.reserve(flagBytes + 64))) return c->fail(SZ4_E_NOMEM, "decoder flags", e);
+  uint32_t* flags = c->unFlags.as<uint32_t>();
+  uint32_t status = 0;
+  if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), keep * sizeof(UnBlock), hipMemcpyHostToDevice, s)) ||
+      (e = hipMemsetAsync(flags, 0, flagBytes, s)))
+    return c->fail(SZ4_E_DEVICE, "decoder plan", e);
+  launch_unlz4_blocks(f, n, c->unBlk.as<UnBlock>(), keep, out, dict, dl, flags, s);
+  if ((e = hipGetLastError()) || (e = hipMemcpyAsync(&status, flags + keep, 4, hipMemcpyDeviceToHost, s)) ||
+      (e = hipStreamSynchronize(s)))
+    return c->fail(SZ4_E_DEVICE, "decode", e);
+  if (status & 2u) return c->fail(SZ4_E_DEVICE, "decoder wait timed out");
+  if (status) return c->fail(SZ4_E_DEVICE, "decoded length differs from the size pass");
+  return SZ4_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -356,7 +424,8 @@ void sz4_destroy(sz4_ctx* c)
   for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
                     &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
                     &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState, &c->longFlag,
-                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong, &c->dictLast, &c->dictPrevH})
+                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong, &c->dictLast, &c->dictPrevH, &c->unBlk,
+                    &c->unMeta, &c->unFlags, &c->unFrame, &c->unDict, &c->unOut})
     b->release();
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
@@ -557,6 +626,53 @@ int sz4_debug_matches(sz4_ctx* c, uint32_t* len, uint16_t* dist, uint64_t n)
   if (hipMemcpy(len, lens.p, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(dist, c->mdist.p, n * 2, hipMemcpyDeviceToHost) != hipSuccess)
     return SZ4_E_DEVICE;
+  return SZ4_OK;
+}
+
+int sz4_unlz4_device(sz4_ctx* c, const void* d_frame, uint64_t frame_len, const void* d_dict, uint64_t dict_len,
+                     void* d_out, uint64_t out_cap, uint64_t* out_size, void* stream)
+{
+  if (!c || !out_size || (!d_frame && frame_len) || (dict_len && !d_dict))
+    return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
+  c->err.clear();
+  hipSetDevice(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  uint64_t total = 0;
+  uint32_t keep = 0;
+  if (int r = unlz4_plan(c, (const uint8_t*)d_frame, frame_len, &total, &keep, s)) return r;
+  *out_size = total;
+  if (total > out_cap || (total && !d_out)) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
+  // the dictionary's last 64 KiB precede the output (smallz4cat.c:168-187)
+  const uint64_t dl = std::min<uint64_t>(dict_len, 65536);
+  const uint8_t* dict = dl ? (const uint8_t*)d_dict + (dict_len - dl) : nullptr;
+  return unlz4_decode(c, (const uint8_t*)d_frame, frame_len, dict, dl, (uint8_t*)d_out, keep, s);
+}
+
+int sz4_unlz4(sz4_ctx* c, const void* frame, uint64_t frame_len, const void* dict, uint64_t dict_len, void* out,
+              uint64_t out_cap, uint64_t* out_size)
+{
+  if (!c || !out_size || (!frame && frame_len) || (dict_len && !dict))
+    return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
+  c->err.clear();
+  hipSetDevice(c->device);
+  hipError_t e;
+  const uint64_t dl = std::min<uint64_t>(dict_len, 65536);
+  if ((e = c->unFrame.reserve(frame_len + 64)) || (e = c->unDict.reserve(dl + 64)))
+    return c->fail(SZ4_E_NOMEM, "staging", e);
+  if ((frame_len && (e = hipMemcpy(c->unFrame.p, frame, frame_len, hipMemcpyHostToDevice))) ||
+      (dl && (e = hipMemcpy(c->unDict.p, (const uint8_t*)dict + (dict_len - dl), dl, hipMemcpyHostToDevice))))
+    return c->fail(SZ4_E_DEVICE, "upload", e);
+  uint64_t total = 0;
+  uint32_t keep = 0;
+  if (int r = unlz4_plan(c, c->unFrame.as<uint8_t>(), frame_len, &total, &keep, nullptr)) return r;
+  *out_size = total;
+  if (total > out_cap || (total && !out)) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
+  if (!total) return SZ4_OK;
+  if ((e = c->unOut.reserve(total))) return c->fail(SZ4_E_NOMEM, "output", e);
+  if (int r = unlz4_decode(c, c->unFrame.as<uint8_t>(), frame_len, dl ? c->unDict.as<uint8_t>() : nullptr, dl,
+                           c->unOut.as<uint8_t>(), keep, nullptr))
+    return r;
+  if ((e = hipMemcpy(out, c->unOut.p, total, hipMemcpyDeviceToHost))) return c->fail(SZ4_E_DEVICE, "download", e);
   return SZ4_OK;
 }
 

@@ -117,4 +117,18 @@ void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
                  uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
                  uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s);
 
+// decoder (sz4_unlz4.hip): one block of an LZ4 frame
+struct UnBlock {
+  uint64_t src;     // payload offset in the frame
+  uint64_t dst;     // output offset (set by the host after the sizes pass)
+  uint64_t size;    // decoded bytes (k_unlz4_sizes), kNone when malformed
+  uint32_t len;     // payload bytes
+  uint32_t stored;  // 1: uncompressed block
+};
+void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s);
+void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, hipStream_t s);
+// flags: nb done flags, then the status word, then the ticket (zeroed before the launch)
+void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, uint8_t* out, const uint8_t* dict,
+                         uint64_t dl, uint32_t* flags, hipStream_t s);
+
 }  // namespace sz4

@@ -69,3 +69,18 @@ def test_cpp_dropin_header_compiles(tmp_path):
     src = os.path.join(ROOT, "tests", "cpp", "dropin_demo.cpp")
     subprocess.run(["g++", "-std=c++11", "-fsyntax-only", "-Wall", "-I", os.path.join(ROOT, "include"), src],
                    check=True)
+
+
+@pytest.mark.skipif(shutil.which("gcc") is None, reason="no gcc")
+def test_c_decoder_dropin_header_compiles():
+    """include/smallz4cat_amd.h (smallz4cat.c's interface over the C ABI) compiles as C99."""
+    src = os.path.join(ROOT, "tests", "cpp", "unlz4_demo.c")
+    subprocess.run(["gcc", "-std=c99", "-fsyntax-only", "-Wall", "-Wextra", "-I", os.path.join(ROOT, "include"), src],
+                   check=True)
+
+
+def test_decoder_rejects_null_context():
+    lib = _native.lib()
+    size = ctypes.c_uint64()
+    assert lib.sz4_unlz4(None, b"x", 1, None, 0, None, 0, ctypes.byref(size)) == -1
+    assert lib.sz4_unlz4_device(None, None, 0, None, 0, None, 0, ctypes.byref(size), None) == -1

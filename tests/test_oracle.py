@@ -117,3 +117,49 @@ def test_oz_block_is_frame_body():
     data = synth.enwik8_like(65536, seed=3)
     frame = pyoracle.oz_lz4(data, 65535)
     assert pyoracle.oz_block(data, 65535) == frame[7:-4]
+
+
+def _flag_frame(flags, frame):
+    """Re-wrap the blocks of a 7-byte-header modern frame with descriptor FLG `flags` (content size,
+    dictionary ID, block and content checksums filled with arbitrary bytes: the decoder skips them)."""
+    import struct
+    pos, body = 7, b""
+    while True:
+        word = int.from_bytes(frame[pos:pos + 4], "little")
+        pos += 4
+        if word == 0:
+            break
+        n = word & 0x7FFFFFFF
+        body += frame[pos - 4:pos + n] + (b"\xDE\xAD\xBE\xEF" if flags & 16 else b"")
+        pos += n
+    hdr = frame[:4] + bytes([flags, 0x70]) + (struct.pack("<Q", 7) if flags & 8 else b"") + \
+        (b"\x11\x22\x33\x44" if flags & 1 else b"") + b"\xAB"
+    return hdr + body + b"\0\0\0\0" + (b"\x01\x02\x03\x04" if flags & 4 else b"")
+
+
+@pytest.mark.skipif(not os.path.exists(pyoracle.REF_CAT), reason="reference decoder not compiled")
+def test_decoder_oracle_matches_reference_binary(tmp_path):
+    """oz_unlz4 -- the checker of the device decoder -- against the reference's own smallz4cat: the
+    same bytes on valid frames (descriptor fields, stored and legacy blocks, a >= 64 KiB dictionary),
+    and both reject signature, version, truncation and offset-0 errors.  Not compared: references
+    before the history (the reference reads uninitialised memory) and tokens that run past their
+    block (the reference reads on into the next block; oz_unlz4 and the device reject them)."""
+    data = synth.enwik8_like(150000, seed=80) + synth.random_bytes(30000, seed=81)
+    dic = synth.enwik8_like(70000, seed=82)
+    (tmp_path / "d").write_bytes(dic)
+    m = pyoracle.oz_lz4(data, 9)
+    valid = [(m, None), (pyoracle.oz_lz4(data, 0), None), (pyoracle.oz_lz4(data, 6, b"", True), None),
+             (_flag_frame(0x5D, m), None), (_flag_frame(0x48, m), None),
+             (pyoracle.oz_lz4(data[:60000], 7, dic), str(tmp_path / "d"))]
+    for frame, d in valid:
+        ref = subprocess.run([pyoracle.REF_CAT] + (["-D", d] if d else []), input=frame, capture_output=True)
+        assert ref.returncode == 0
+        assert ref.stdout == pyoracle.oz_unlz4(frame, dic if d else b"")
+    hdr = bytes([4, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF])
+    bad = [b"\x00\x22\x4d\x18" + m[4:], bytes([4, 0x22, 0x4D, 0x18, 0x00, 0x70, 0xDF, 0, 0, 0, 0]),
+           hdr + b"\x04\0\0\0" + b"\x10a\x00\x00" + b"\0\0\0\0", m[:len(m) // 2], m[:-4], m[:5]]
+    for frame in bad:
+        ref = subprocess.run([pyoracle.REF_CAT], input=frame, capture_output=True)
+        assert ref.returncode == 1
+        with pytest.raises(ValueError):
+            pyoracle.oz_unlz4(frame)
