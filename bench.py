@@ -33,7 +33,7 @@ from smallz4_amd import synth  # noqa: E402  (input generators; the HIP library 
 
 METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01d_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01g_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
 
 # input shapes (smallz4_amd/synth.py); the default is the headline workload (configs[1])
 DATA = {
@@ -195,18 +195,21 @@ def main():
 
     if rank == 0:
         value = world * nbytes * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel k_find_sorted: its compulsory HBM bytes
-        # per searched position = text byte (1) + sorted slot arrays, u16 position and group start (4)
-        # + match written, u32 length and u16 distance (6) = 11
+        # roofline of the dominant kernel k_find_sorted.  Its compulsory HBM bytes
+        # per position: text byte (1) + sorted slot arrays, u16 position and group start (4, read; with
+        # the sort fused in, written) + match, u32 length and u16 distance (6, written); fused, also
+        # the rank of every target (4, written)
+        fused = os.environ.get("SZ4_FUSE_SORT", "") == "1"
         find_ms = stages.get("find_sorted", 0.0)
         targets = sum(max(0, min(args.block_size, nbytes - o) - 11) for o in range(0, nbytes, args.block_size))
-        alg_bytes = nbytes + 4 * nbytes + 6 * targets
+        alg_bytes = nbytes + 4 * nbytes + 6 * targets + (4 * targets if fused else 0)
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
         traffic = None
         default_cfg = args.data == "enwik8" and args.block_size == 65536 and args.level == 9 and nbytes == 100_000_000
-        if default_cfg and os.path.exists(PMC_FILE):
+        if default_cfg and fused and os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        kname = "k_find_sorted (k_sort fused in)" if fused else "k_find_sorted"
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -229,7 +232,7 @@ def main():
             "verified_against": kind,
             "compression_ratio": round(size / nbytes, 5),
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
-            "roofline": {"kernel": "k_find_sorted", "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+            "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
                          "algorithmic_bytes_per_launch": alg_bytes},
         }

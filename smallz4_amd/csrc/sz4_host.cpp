@@ -84,6 +84,7 @@ struct sz4_ctx {
   uint32_t lastBlocks = 0;
   int stopAfter = 0;
   uint32_t lastChain = 0;
+  bool separateSort = true;  // k_sort as its own launch; SZ4_FUSE_SORT=1 runs it inside k_find_sorted
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
@@ -264,22 +265,25 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   // another sort/find/prep round (each round checks a longer prefix of it)
   for (uint32_t round = 0; c->dictBack < 0; round++) {
     if (maxChain > 0) {
-      launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
       // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
       if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
           (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
         return c->fail(SZ4_E_DEVICE, "clear matches", e);
+      // with SZ4_FUSE_SORT=1 k_find_sorted sorts its own segment first
+      if (c->separateSort)
+        launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
     }
     mark(c, 2, s);
     if (maxChain > 0)
       launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                  nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, s);
+                  nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, !c->separateSort, s);
     mark(c, 3, s);
     if (maxChain > 0)
       launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                  c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds, s);
+                  c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds,
+                  false, s);
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel.as<uint32_t>(),
@@ -408,6 +412,8 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   if (hipSetDevice(device) != hipSuccess) return SZ4_E_DEVICE;
   sz4_ctx* c = new sz4_ctx();
   c->device = device;
+  const char* fuse = getenv("SZ4_FUSE_SORT");
+  c->separateSort = !(fuse && fuse[0] == '1');
   for (auto& e : c->ev) hipEventCreate(&e);
   if (reserve_bytes && c->staged.reserve(reserve_bytes + kPad) != hipSuccess) {
     sz4_destroy(c);

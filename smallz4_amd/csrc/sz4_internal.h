@@ -90,15 +90,16 @@ void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Inter
 void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
                  uint32_t* rank, hipStream_t s);
-// pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals)
+// pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals); fuseSort: pass 1 runs
+// k_sort's work for its segment first (compact = sorted slot arrays, scratch = sort buffer, rank written)
 // scratch: per-slot words free after k_sort (the skip pointers of k_find_long9); longBits: one bit per
 // position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target;
 // specLen/specDist: per position words free before the parse (speculative carries of pass-2 piece heads)
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
-                 const Interval* iv, const uint32_t* ivCount, const uint2* compact, uint2* scratch,
-                 const uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
+                 const Interval* iv, const uint32_t* ivCount, uint2* compact, uint2* scratch,
+                 uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
-                 bool ldsWindow, uint32_t hybridLds, hipStream_t s);
+                 bool ldsWindow, uint32_t hybridLds, bool fuseSort, hipStream_t s);
 // dictionary mode: one wavefront replays the reference's match loop (dictBack = first insertion offset
 // before the first block); last: 2^20 u32 scratch, prevH: 65536 u16 scratch
 void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,

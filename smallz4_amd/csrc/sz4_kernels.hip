@@ -348,19 +348,26 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
   return (key * 2654435761u) >> posBits;  // top (32 - posBits) bits of a multiplicative hash
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
-                                                       const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
-                                                       const uint32_t* __restrict__ ivCount, uint2* __restrict__ bufA,
-                                                       uint2* __restrict__ bufB, uint32_t* __restrict__ rank)
-{
-  __shared__ uint32_t hist[kSortWaves][256];
-  __shared__ uint32_t wsum[4];
-  __shared__ uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
-  __shared__ uint32_t nEx;
-  __shared__ uint32_t s_scan[kSortThreads];
+// k_sort's shared memory.  When k_find_sorted sorts its own segment it lives in the window buffer,
+// which is loaded only after the sort.
+struct SortLds {
+  uint32_t hist[kSortWaves][256];
+  uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
+  uint32_t scan[kSortThreads];
+  uint32_t wsum[4];
+  uint32_t nEx;
+};
 
-  const Segment S = segs[blockIdx.x];
-  const Block B = blocks[S.block];
+__device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, const Segment& S, const Block& B,
+                                             const Interval* __restrict__ ivAll, const uint32_t* __restrict__ ivCount,
+                                             uint2* bufA, uint2* bufB, uint32_t* rank, SortLds& L)
+{
+  auto& hist = L.hist;
+  auto& wsum = L.wsum;
+  auto& exLo = L.exLo;
+  auto& exHi = L.exHi;
+  auto& nEx = L.nEx;
+  auto& s_scan = L.scan;
   const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
 
   // positions excluded from insertion: shortcut intervals of this block and of the previous one
@@ -527,6 +534,17 @@ __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict
   }
 }
 
+__global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                       const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                       const uint32_t* __restrict__ ivCount, uint2* __restrict__ bufA,
+                                                       uint2* __restrict__ bufB, uint32_t* __restrict__ rank)
+{
+  __shared__ SortLds lds;
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  sort_segment(in, S, B, ivAll, ivCount, bufA, bufB, rank, lds);
+}
+
 // ================================================================================================
 // k_find: longest match per target position.  One workgroup per segment; wavefronts take chunks
 // of 64 consecutive positions and walk them in order.  For each position the wavefront scores
@@ -631,10 +649,11 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 template <bool kLds>
 __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96))) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                               const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
-                                                              const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
+                                                              const uint32_t* __restrict__ ivCount, uint2* compactAll,
                                                               uint32_t maxChain, uint32_t* __restrict__ mlen,
                                                               uint16_t* __restrict__ mdist, uint64_t matchBase,
-                                                              uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong)
+                                                              uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong,
+                                                              uint2* sortA, uint32_t* rankOut, uint32_t fuseSort)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
@@ -666,6 +685,13 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
   }
   const uint32_t E = W - excluded;
   const bool small = compact_small(S);
+  if (fuseSort) {
+    // k_sort's work for this segment first, its shared memory in the (not yet loaded) window
+    // buffer: the latency-bound sort of one workgroup overlaps the issue-bound search of the other
+    // workgroup on the CU, and the sorted slots it writes are read back while L2-warm
+    sort_segment(in, S, B, ivAll, ivCount, sortA, compactAll, rankOut, *reinterpret_cast<SortLds*>(win));
+    __syncthreads();
+  }
 
 #if SZ4_DIAG == 3
   const uint64_t t0 = __builtin_readcyclecounter();
@@ -3302,11 +3328,12 @@ uint32_t find_lds_bytes() { return 65536 + 16; }
 uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
-                 const uint32_t* ivCount, const uint2* compact, uint2* scratch, const uint32_t* rank, uint32_t maxChain,
+                 const uint32_t* ivCount, uint2* compact, uint2* scratch, uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* longBits, uint32_t* segLong,
                  uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist, bool ldsWindow, uint32_t hybridLds,
-                 hipStream_t s)
+                 bool fuseSort, hipStream_t s)
 {
+  static_assert(sizeof(SortLds) <= 65536, "the fused sort's shared memory must fit the window buffer");
   if (!nsegs) return;
   const bool unlimited = maxChain >= 65535u;
   if (ldsWindow) {
@@ -3319,7 +3346,8 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     }
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
-                         ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong);
+                         ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank,
+                         (uint32_t)fuseSort);
     else if (unlimited)
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
@@ -3336,7 +3364,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
         attrBytes1 = hybridLds;
       }
       hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
-                         compact, maxChain, mlen, mdist, matchBase, longBits, segLong);
+                         compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {
       static uint32_t attrBytes = 0;

@@ -163,3 +163,13 @@ def test_decoder_oracle_matches_reference_binary(tmp_path):
         assert ref.returncode == 1
         with pytest.raises(ValueError):
             pyoracle.oz_unlz4(frame)
+
+
+@pytest.mark.skipif(not os.path.exists(pyoracle.REF_CAT), reason="reference decoder not compiled")
+def test_reference_legacy_level0_loses_data():
+    """Pins a reference defect: a legacy frame at level 0 carries an empty block (no literals), and
+    the reference's smallz4cat decodes it to nothing; oz_unlz4 and the device decoder agree."""
+    frame = pyoracle.ref_lz4(b"abcdefgh" * 100, 0, b"", True)
+    assert frame == bytes.fromhex("02214c1800000000")
+    out = subprocess.run([pyoracle.REF_CAT], input=frame, capture_output=True, check=True).stdout
+    assert out == b"" == pyoracle.oz_unlz4(frame)

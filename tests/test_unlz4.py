@@ -78,7 +78,11 @@ def test_unlz4_golden_streams(compressor, golden):
         frame = compressor.lz4(data, case["level"], dictionary, bool(case["legacy"]))
         assert inputs.sha(frame) == case["out_sha256"]
         got = check(compressor, frame, dictionary)
-        if not dictionary:
+        if case["legacy"] and case["level"] == 0:
+            # the reference writes an empty block for a legacy frame at level 0, and its smallz4cat
+            # decodes that to nothing (a reference defect, reproduced: tests/test_oracle.py)
+            assert got == b"", case["name"]
+        elif not dictionary:
             assert got == data, (case["name"], case["level"], case["legacy"])
 
 
