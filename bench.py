@@ -33,7 +33,7 @@ from smallz4_amd import synth  # noqa: E402  (input generators; the HIP library 
 
 METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01g_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
+PMC_FILE = os.path.join(ROOT, "profiles", "r01h_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
 
 # input shapes (smallz4_amd/synth.py); the default is the headline workload (configs[1])
 DATA = {
@@ -199,7 +199,7 @@ def main():
         # per position: text byte (1) + sorted slot arrays, u16 position and group start (4, read; with
         # the sort fused in, written) + match, u32 length and u16 distance (6, written); fused, also
         # the rank of every target (4, written)
-        fused = os.environ.get("SZ4_FUSE_SORT", "") == "1"
+        fused = os.environ.get("SZ4_SEPARATE_SORT", "") != "1"
         find_ms = stages.get("find_sorted", 0.0)
         targets = sum(max(0, min(args.block_size, nbytes - o) - 11) for o in range(0, nbytes, args.block_size))
         alg_bytes = nbytes + 4 * nbytes + 6 * targets + (4 * targets if fused else 0)

@@ -84,7 +84,7 @@ struct sz4_ctx {
   uint32_t lastBlocks = 0;
   int stopAfter = 0;
   uint32_t lastChain = 0;
-  bool separateSort = true;  // k_sort as its own launch; SZ4_FUSE_SORT=1 runs it inside k_find_sorted
+  bool separateSort = false;  // k_sort runs inside k_find_sorted; SZ4_SEPARATE_SORT=1: its own launch
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
@@ -269,7 +269,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
       if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
           (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
         return c->fail(SZ4_E_DEVICE, "clear matches", e);
-      // with SZ4_FUSE_SORT=1 k_find_sorted sorts its own segment first
+      // k_find_sorted sorts its own segment first unless SZ4_SEPARATE_SORT=1
       if (c->separateSort)
         launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
     }
@@ -412,8 +412,8 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   if (hipSetDevice(device) != hipSuccess) return SZ4_E_DEVICE;
   sz4_ctx* c = new sz4_ctx();
   c->device = device;
-  const char* fuse = getenv("SZ4_FUSE_SORT");
-  c->separateSort = !(fuse && fuse[0] == '1');
+  const char* sep = getenv("SZ4_SEPARATE_SORT");
+  c->separateSort = sep && sep[0] == '1';
   for (auto& e : c->ev) hipEventCreate(&e);
   if (reserve_bytes && c->staged.reserve(reserve_bytes + kPad) != hipSuccess) {
     sz4_destroy(c);
