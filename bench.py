@@ -2,26 +2,46 @@
 """bench.py -- BASELINE.json's metric on MI355X.
 
 metric : input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)
-workload (BASELINE configs[1]): enwik8-shaped input (100 MB per GPU, synthetic --
-    enwik8 itself is not available offline) compressed as independent 64 KiB
-    blocks at -9 (maxChainLength 65535).  One step = one full compression of the
-    rank's 100 MB, input resident in HBM, frame written to HBM.
-multi-GPU: one process per GPU; blocks shard with no data-path collective
-    (weak scaling: every rank compresses its own 100 MB).  The barrier and the
-    max-over-ranks timing are the only collectives.
+
+workloads (BASELINE.json configs; all synthetic, the corpora are not available offline):
+  enwik8        configs[1]: 100 MB enwik8-shaped text, independent 64 KiB blocks, -9.  The default at
+                N=1 (the configuration the metric is quoted on).
+  enwik9        configs[3]: an enwik9-shaped input (10^9 bytes at 8 GPUs) in 64 KiB blocks, sharded:
+                rank r of N compresses its contiguous block range of the first N x 125 MB, so every
+                GPU does the same work at any N (weak scaling) and N=8 is the whole 10^9 bytes.  The
+                default at N>1.
+  zeros_urandom configs[4]: 10 GiB of alternating 128 KiB zero / urandom runs at 8 GPUs, 256 KiB
+                blocks, sharded the same way (1.25 GiB per GPU).
+  silesia       configs[2]: Silesia-shaped mixed content (text, XML, executables, database rows,
+                images, source), 4 MiB independent blocks, 1 GPU.
+One step = one full compression of the rank's shard, input resident in HBM, blocks written to HBM.
+
+multi-GPU: one process per GPU.  Blocks are independent, so ranks shard the block range of ONE input
+(smallz4_amd/shard.py) with no data-path collective; each rank's part (bare blocks; rank 0 adds the
+header, the last rank the end mark) concatenates to the single-GPU frame.  The barrier, the
+max-over-ranks time and the result reductions are the only collectives.  `--gpus N` without a
+torch.distributed environment starts N ranks itself (a torch.distributed.run child process, before
+this process touches the GPU) and exits with its status.
 
 Also reported:
-  byte_diff     differing bytes between the GPU frame and the reference's output for
-                every block (oracle/_ref, compiled from the reference sources; the C
-                restatement when _ref is absent), all blocks, every rank
-  roofline      dominant kernel (k_find_sorted), HIP-event timed on its stream
-  cpu_baseline  the reference itself on this host, one thread, bounded sample
+  byte_diff      differing bytes between the GPU blocks and the reference's output for the same
+                 blocks (oracle/_ref, compiled from the reference sources; the C restatement when
+                 _ref is absent): every block at N=1 on enwik8, a fixed per-rank sample otherwise
+  roundtrip      every rank's part decoded on the device (sz4_unlz4_device) equals its input
+  roofline       dominant kernel (k_find_sorted), HIP-event timed on its stream; HBM traffic from the
+                 newest matching profiles/*_pmc.json (rocprofv3 PMC passes of the same workload)
+  cpu_baseline   the reference itself on this host: all 16 host threads of the box's share, and one
+                 thread, on a bounded sample
+  stream         sz4_lz4 (the drop-in's host-buffer path: 4 MiB dependent blocks, chunked, PCIe
+                 included), 1 GPU, outside the timed region
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import subprocess
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -29,114 +49,230 @@ from concurrent.futures import ThreadPoolExecutor
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from smallz4_amd import synth  # noqa: E402  (input generators; the HIP library loads lazily)
+from smallz4_amd import shard, synth  # noqa: E402  (input generators; the HIP library loads lazily)
 
 METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0)"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
-PMC_FILE = os.path.join(ROOT, "profiles", "r01h_find_hbm_bytes.json")  # k_find_sorted HBM bytes (summarize.py)
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max clock
+SIMDS, CUS = 1024, 256  # 256 CUs x 4 SIMDs
+HOST_THREADS = 16       # the GPU box's CPU share per GPU (gpurun) -- the all-cores baseline
 
-# input shapes (smallz4_amd/synth.py); the default is the headline workload (configs[1])
-DATA = {
-    "enwik8": ("synthetic enwik8-shaped text (smallz4_amd/synth.py; enwik8 is not available offline)",
-               lambda n, seed: synth.enwik8_like(n, seed=seed)),
-    "zeros_urandom": ("synthetic: alternating 128 KiB runs of zeros and urandom bytes (configs[4]'s two extremes)",
-                      lambda n, seed: synth.zeros_urandom(n, seed=seed)),
-    "zeros": ("synthetic: all zero bytes", lambda n, seed: bytes(n)),
-    "random": ("synthetic: urandom bytes (numpy, seeded)", lambda n, seed: synth.random_bytes(n, seed=seed)),
+# name -> (BASELINE config, description, block size, bytes per rank at N ranks, range generator)
+WORKLOADS = {
+    "enwik8": ("configs[1]", "synthetic enwik8-shaped text (smallz4_amd/synth.py; enwik8 is not available offline)",
+               65536, lambda world: 100_000_000,
+               lambda lo, hi: synth.enwik8_like(100_000_000, seed=8)[lo:hi]),
+    "enwik9": ("configs[3]", "synthetic enwik9-shaped text: 16 MiB enwik8-shaped segments (synth.enwik9_like_range)",
+               65536, lambda world: 125_000_000,
+               lambda lo, hi: synth.enwik9_like_range(lo, hi, seed=9, workers=4)),
+    "zeros_urandom": ("configs[4]", "synthetic: alternating 128 KiB runs of zeros and urandom bytes (synth.zeros_urandom_range)",
+                      262144, lambda world: (10 << 30) // 8,
+                      lambda lo, hi: synth.zeros_urandom_range(lo, hi, seed=10)),
+    "silesia": ("configs[2]", "synthetic Silesia-shaped mixed content (synth.silesia_like; the corpus is not available offline)",
+                4 << 20, lambda world: 211_938_580,
+                lambda lo, hi: synth.silesia_like(hi, seed=2)[lo:hi]),
 }
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--mb", type=float, default=100.0, help="input MB (1e6 bytes) per GPU")
-    ap.add_argument("--block-size", type=int, default=65536)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: enwik8 (configs[1]) at one GPU, enwik9 (configs[3]) at several")
+    ap.add_argument("--mb", type=float, default=None, help="override: input MB (1e6 bytes) per rank")
+    ap.add_argument("--block-size", type=int, default=None, help="override the workload's block size")
     ap.add_argument("--level", type=int, default=9)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
-    ap.add_argument("--verify-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU baseline sample")
+    ap.add_argument("--verify-threads", type=int, default=HOST_THREADS)
+    ap.add_argument("--verify-blocks", type=int, default=256,
+                    help="per-rank sample of blocks diffed against the reference (0 = every block)")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-decode", action="store_true", help="skip the decoder leg (sz4_unlz4_device)")
-    ap.add_argument("--data", default="enwik8", choices=sorted(DATA),
-                    help="synthetic input shape (enwik8: configs[1]; zeros_urandom: configs[4])")
-    return ap.parse_args()
+    ap.add_argument("--no-decode", action="store_true", help="skip the device round trip (sz4_unlz4_device)")
+    ap.add_argument("--no-stream", action="store_true", help="skip the sz4_lz4 host-buffer leg")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: gloo ranks compress their shards with the oracle (tests the sharding)")
+    a = ap.parse_args(argv)
+    if a.workload is None:
+        a.workload = "enwik8" if a.gpus == 1 else "enwik9"
+    return a
 
 
-def expected_blocks(data: bytes, bs: int, chain: int, threads: int):
-    """Per-block reference output (block word + payload), computed on the CPU."""
+def rank_range(args, world, rank):
+    """(global input length, [lo, hi) of this rank, block size)."""
+    wl = WORKLOADS[args.workload]
+    bs = args.block_size or wl[2]
+    per = int(args.mb * 1e6) if args.mb else wl[3](world)
+    total = per * world
+    lo, hi = shard.shard_range(total, bs, rank, world)
+    return total, lo, hi, bs
+
+
+def expected_blocks(data: bytes, bs: int, chain: int, threads: int, offsets):
+    """Reference output (block word + payload) of the blocks starting at `offsets`, on the CPU."""
     from oracle import pyoracle
     if pyoracle.ref_available():
         def one(off):
-            f = pyoracle.ref_lz4(data[off:off + bs], chain)
-            return f[7:-4]
+            return pyoracle.ref_lz4(data[off:off + bs], chain)[7:-4]
         kind = "reference"
     else:
         def one(off):
             return pyoracle.oz_block(data[off:off + bs], chain)
         kind = "port"
     with ThreadPoolExecutor(max_workers=threads) as ex:
-        parts = list(ex.map(one, range(0, len(data), bs)))
-    return parts, kind
+        return list(ex.map(one, offsets)), kind
 
 
-def byte_diff(frame: bytes, parts, header: bytes) -> int:
-    expect = header + b"".join(parts) + b"\0\0\0\0"
-    n = min(len(frame), len(expect))
-    import numpy as np
-    a = np.frombuffer(frame[:n], dtype=np.uint8)
-    b = np.frombuffer(expect[:n], dtype=np.uint8)
-    return int((a != b).sum()) + abs(len(frame) - len(expect))
+def block_spans(part: bytes):
+    """(offset, length) of every block (word + payload) in a run of bare blocks."""
+    spans, pos = [], 0
+    while pos + 4 <= len(part):
+        word = int.from_bytes(part[pos:pos + 4], "little")
+        n = 4 + (word & 0x7FFFFFFF)
+        spans.append((pos, n))
+        pos += n
+    return spans
+
+
+def sample_diff(part: bytes, data: bytes, bs: int, chain: int, threads: int, sample: int):
+    """Byte diff of a fixed sample of this rank's blocks (every k-th) against the reference."""
+    spans = block_spans(part)
+    nblk = (len(data) + bs - 1) // bs
+    if len(spans) != nblk:
+        return len(part) + 1, 0, None
+    step = 1 if sample <= 0 or nblk <= sample else nblk // sample
+    idx = list(range(0, nblk, step))
+    want, kind = expected_blocks(data, bs, chain, threads, [i * bs for i in idx])
+    diff = 0
+    for i, w in zip(idx, want):
+        o, n = spans[i]
+        got = part[o:o + n]
+        m = min(len(got), len(w))
+        diff += sum(1 for a, b in zip(got[:m], w[:m]) if a != b) if got != w else 0
+        diff += abs(len(got) - len(w))
+    return diff, len(idx), kind
 
 
 def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
+    """The reference (oracle/_ref; the C restatement when absent) on a bounded sample, all threads
+    of the box's share and one thread."""
     from oracle import pyoracle
     if pyoracle.ref_available():
         fn, kind = (lambda b: pyoracle.ref_lz4(b, chain)), "reference"
     else:
         fn, kind = (lambda b: pyoracle.oz_block(b, chain)), "port"
-    done = 0
-    t0 = time.perf_counter()
-    for off in range(0, len(data), bs):
-        fn(data[off:off + bs])
-        done += min(bs, len(data) - off)
-        if time.perf_counter() - t0 >= budget_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": round(done / dt / 1e6, 3), "unit": "MB/s", "cores": 1, "kind": kind,
-            "sample": f"first {done / 1e6:.1f} MB of the rank-0 input as {bs}-byte blocks, level chain={chain}, "
-                      f"one thread, smallz4::lz4 per block ({dt:.1f} s)"}
+    offs = list(range(0, len(data), bs))
+
+    def run(threads):
+        done, t0 = 0, time.perf_counter()
+        with ThreadPoolExecutor(max_workers=threads) as ex:
+            k = 0
+            while k < len(offs) and time.perf_counter() - t0 < budget_s:
+                batch = offs[k:k + threads]
+                for b in ex.map(lambda o: fn(data[o:o + bs]), batch):
+                    pass
+                done += sum(min(bs, len(data) - o) for o in batch)
+                k += len(batch)
+        return done, time.perf_counter() - t0
+
+    done_n, dt_n = run(HOST_THREADS)
+    done_1, dt_1 = run(1)
+    return {"value": round(done_n / dt_n / 1e6, 3), "unit": "MB/s", "cores": HOST_THREADS, "kind": kind,
+            "sample": f"first {done_n / 1e6:.1f} MB of the rank-0 shard as {bs}-byte blocks, maxChainLength {chain}, "
+                      f"smallz4::lz4 per block on {HOST_THREADS} threads ({dt_n:.1f} s)",
+            "single_thread": {"value": round(done_1 / dt_1 / 1e6, 3), "cores": 1,
+                              "sample": f"first {done_1 / 1e6:.1f} MB, one thread ({dt_1:.1f} s)"}}
+
+
+def pmc_traffic(cfg):
+    """HBM bytes per k_find_sorted launch from the newest profiles/*_pmc.json of this workload."""
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if rec.get("config") == cfg:
+            best = (path, rec)
+    return best
+
+
+def spawn_ranks(args):
+    """`--gpus N` outside torch.distributed: run N ranks through torch.distributed.run as a child
+    process (this process has not touched the GPU) and return its exit status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """HIP-free rehearsal of the sharded path (gloo): each rank compresses its block range with the
+    oracle; rank 0 checks that the parts concatenate to the single-process frame."""
+    import torch.distributed as dist
+    from oracle import pyoracle
+    if world > 1:
+        dist.init_process_group("gloo")
+    total, lo, hi, bs = rank_range(args, world, rank)
+    data = WORKLOADS[args.workload][4](lo, hi)
+    chain = 65535 if args.level == 9 else args.level
+    body = b"".join(pyoracle.oz_block(data[o:o + bs], chain) for o in range(0, len(data), bs))
+    part = shard.frame_part(body, rank, world)
+    frame = shard.gather_frame(part) if world > 1 else part
+    if rank == 0:
+        whole = WORKLOADS[args.workload][4](0, total)
+        single = shard.HEADER + b"".join(pyoracle.oz_block(whole[o:o + bs], chain)
+                                         for o in range(0, total, bs)) + shard.END_MARK
+        print(json.dumps({"dry_run": True, "n_gpus": world, "workload": args.workload, "input_bytes": total,
+                          "frame_bytes": len(frame), "parts_equal_single": frame == single}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse_args()
-    import torch
-    import torch.distributed as dist
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        return dry_run(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
-
     import smallz4_amd
 
     chain = smallz4_amd.level_to_chain(args.level)
-    nbytes = int(args.mb * 1e6)
-    data = DATA[args.data][1](nbytes, 8 + rank)
-    t_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda(local)
+    total, lo, hi, bs = rank_range(args, world, rank)
+    nbytes = hi - lo
+    data = WORKLOADS[args.workload][4](lo, hi)
+    dev = f"cuda:{local}"
+    t_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if nbytes else torch.empty(0, dtype=torch.uint8, device=dev)
     comp = smallz4_amd.Compressor(device=local)
-    cap = comp._lib.sz4_bound(nbytes, args.block_size)
-    out = torch.empty(cap, dtype=torch.uint8, device=f"cuda:{local}")
+    cap = comp._lib.sz4_bound(nbytes, bs)
+    out = torch.empty(max(cap, 16), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream(local).cuda_stream
+    # rank 0 writes the smallz4 header, the last rank the end mark, the others bare blocks
+    header = "smallz4" if world == 1 else "none"
 
     def step():
-        return comp.compress_blocks_device(t_in.data_ptr(), nbytes, out.data_ptr(), cap, args.block_size, chain,
-                                           "smallz4", stream)
+        return comp.compress_blocks_device(t_in.data_ptr(), nbytes, out.data_ptr(), cap, bs, chain, header, stream)
 
     comp.set_timing(True)
     for _ in range(args.warmup):
@@ -157,59 +293,97 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(local)
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     stages = {k: v / args.steps for k, v in stage_sum.items()}
-    frame = out[:size].cpu().numpy().tobytes()
+    part = out[:size].cpu().numpy().tobytes()
+    blocks = part[7:-4] if header == "smallz4" else part
 
-    # decoder leg (smallz4cat semantics on the device, sz4_unlz4_device), outside the timed region:
-    # the frame just written, decoded back into HBM and compared with the input
-    dec = None
-    if not args.no_decode:
-        dout = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
-        comp.unlz4_device(out.data_ptr(), size, dout.data_ptr(), nbytes, stream=stream)
+    # device round trip of this rank's part (outside the timed region): wrap the bare blocks as a
+    # frame on the device, decode with sz4_unlz4_device, compare with the input in HBM
+    rt_ok, dec = True, None
+    if not args.no_decode and nbytes:
+        fr = torch.empty(len(blocks) + 11, dtype=torch.uint8, device=dev)
+        fr[:7] = torch.tensor(list(shard.HEADER), dtype=torch.uint8)
+        off = 7 if header == "smallz4" else 0
+        fr[7:7 + len(blocks)] = out[off:off + len(blocks)]
+        fr[7 + len(blocks):] = 0
+        dout = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), nbytes, stream=stream)
         torch.cuda.synchronize(local)
         reps = 3
-        t0 = time.perf_counter()
+        td = time.perf_counter()
         for _ in range(reps):
-            got = comp.unlz4_device(out.data_ptr(), size, dout.data_ptr(), nbytes, stream=stream)
+            got = comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), nbytes, stream=stream)
         torch.cuda.synchronize(local)
-        dt = (time.perf_counter() - t0) / reps
-        dec = {"value": round(nbytes / dt / 1e6, 1), "unit": "MB/s of decoded output (host-timed call: index, "
-               "sizes and decode launches with their syncs)", "ms": round(dt * 1e3, 3),
-               "roundtrip_equal": bool(got == nbytes and torch.equal(dout, t_in))}
-        del dout
+        dt = (time.perf_counter() - td) / reps
+        rt_ok = bool(got == nbytes and torch.equal(dout, t_in))
+        dec = {"value": round(nbytes / dt / 1e6, 1), "unit": "MB/s of decoded output (rank 0; host-timed call: "
+               "index, sizes and decode launches with their syncs)", "ms": round(dt * 1e3, 3)}
+        del dout, fr
 
-    # output-byte diff against the reference, every block of every rank
+    # output-byte diff against the reference on a sample of this rank's blocks (all at N=1 on enwik8)
     diff, verified, kind = -1, 0, None
-    if not args.no_verify:
-        parts, kind = expected_blocks(data, args.block_size, chain, args.verify_threads)
-        diff = byte_diff(frame, parts, bytes([0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF]))
-        verified = len(parts)
-        if world > 1:
-            t = torch.tensor([diff, verified], dtype=torch.int64, device=f"cuda:{local}")
-            dist.all_reduce(t)
-            diff, verified = int(t[0]), int(t[1])
+    if not args.no_verify and nbytes:
+        sample = 0 if (world == 1 and args.workload == "enwik8") else args.verify_blocks
+        diff, verified, kind = sample_diff(blocks, data, bs, chain, args.verify_threads, sample)
+
+    # whole-job results over ranks
+    res = torch.tensor([elapsed, float(size), float(diff), float(verified), 0.0 if rt_ok else 1.0],
+                       dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = res.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(res, op=dist.ReduceOp.SUM)
+        elapsed = float(mx[0])
+        frame_bytes = int(res[1]) + 11
+        diff = -1 if float(mx[2]) < 0 else int(res[2])
+        verified, rt_bad = int(res[3]), int(res[4])
+    else:
+        frame_bytes, rt_bad = size, 0 if rt_ok else 1
+
+    stream_leg = None
+    if world == 1 and not args.no_stream and nbytes:
+        # the drop-in's host-buffer path (4 MiB dependent blocks, chunked; PCIe included)
+        sdata = data[:min(nbytes, 100_000_000)]
+        comp.lz4(sdata[:1 << 20], chain)
+        ts = time.perf_counter()
+        sframe = comp.lz4(sdata, chain)
+        dts = time.perf_counter() - ts
+        stream_leg = {"value": round(len(sdata) / dts / 1e6, 1), "unit": "MB/s (host buffers in and out, PCIe included)",
+                      "input_bytes": len(sdata), "ratio": round(len(sframe) / len(sdata), 5),
+                      "path": "sz4_lz4: smallz4::lz4 stream semantics, 4 MiB dependent blocks, 64 MiB chunks",
+                      "device_bytes": comp.device_bytes()}
 
     if rank == 0:
-        value = world * nbytes * args.steps / elapsed / 1e6
-        # roofline of the dominant kernel k_find_sorted.  Its compulsory HBM bytes
-        # per position: text byte (1) + sorted slot arrays, u16 position and group start (4, read; with
-        # the sort fused in, written) + match, u32 length and u16 distance (6, written); fused, also
-        # the rank of every target (4, written)
-        fused = os.environ.get("SZ4_SEPARATE_SORT", "") != "1"
+        wl = WORKLOADS[args.workload]
+        value = total * args.steps / elapsed / 1e6
+        cfg = {"workload": f"{args.workload} ({wl[0]}): {total / 1e6:g} MB as independent {bs}-byte blocks, "
+                           f"level -{args.level} (maxChainLength {chain}), {nbytes / 1e6:g} MB per GPU",
+               "baseline_config": wl[0], "block_size": bs, "level": args.level, "input_bytes": total,
+               "bytes_per_gpu": nbytes, "parallelism": f"block ranges of one input sharded over {world} GPU(s), "
+                                                      "no data-path collective"}
+        # dominant kernel k_find_sorted (the sort fused in).  Algorithmic bytes per position: text byte
+        # (1) + the sorted slot arrays written and read back (4 + 4: u16 position and group start) +
+        # the match written (6: u32 length, u16 distance) = 15 B
         find_ms = stages.get("find_sorted", 0.0)
-        targets = sum(max(0, min(args.block_size, nbytes - o) - 11) for o in range(0, nbytes, args.block_size))
-        alg_bytes = nbytes + 4 * nbytes + 6 * targets + (4 * targets if fused else 0)
+        alg_bytes = 15 * nbytes
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
-        traffic = None
-        default_cfg = args.data == "enwik8" and args.block_size == 65536 and args.level == 9 and nbytes == 100_000_000
-        if default_cfg and fused and os.path.exists(PMC_FILE):
-            with open(PMC_FILE) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        kname = "k_find_sorted (k_sort fused in)" if fused else "k_find_sorted"
+        pmc_cfg = {"workload": args.workload, "bytes_per_gpu": nbytes, "block_size": bs, "level": args.level}
+        pmc = pmc_traffic(pmc_cfg)
+        roof = {"kernel": "k_find_sorted (k_sort fused in)", "bound": "hbm", "achieved": round(achieved, 3),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": pmc[1]["hbm_bytes_per_launch"] if pmc else None,
+                "algorithmic_bytes_per_launch": alg_bytes,
+                "limiter": "issue/latency: the kernel checks every candidate of the reference's -9 hash chain "
+                           "(DESIGN.md section 6); the HBM roofline fraction says how far it is from being "
+                           "memory bound",
+                "step_compulsory": {"bytes": nbytes + size, "GB/s": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world, 3),
+                                    "frac": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world / HBM_PEAK_GBS, 6),
+                                    "note": "input read + frame written per GPU per step over the whole step"}}
+        if pmc:
+            roof["traffic_source"] = os.path.relpath(pmc[0], ROOT)
+            for k in ("valu_per_simd_cycle", "salu_per_cu_cycle", "avg_duration_us"):
+                if k in pmc[1]:
+                    roof[k] = pmc[1][k]
         rec = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -222,24 +396,22 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": DATA[args.data][0],
-            "config": {"workload": f"{args.data}-shaped {args.mb:g} MB per GPU as independent {args.block_size}-byte "
-                                   f"blocks, level -{args.level} (maxChainLength {chain})",
-                       "block_size": args.block_size, "level": args.level, "bytes_per_gpu": nbytes,
-                       "parallelism": f"blocks sharded over {world} GPU(s), no data-path collective"},
+            "data": wl[1],
+            "config": cfg,
             "byte_diff": diff,
             "blocks_verified": verified,
             "verified_against": kind,
-            "compression_ratio": round(size / nbytes, 5),
+            "roundtrip_ok": rt_bad == 0,
+            "compression_ratio": round(frame_bytes / total, 5) if total else None,
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
-            "roofline": {"kernel": kname, "bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": traffic,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+            "roofline": roof,
         }
         if dec is not None:
             rec["unlz4"] = dec
+        if stream_leg is not None:
+            rec["stream"] = stream_leg
         if world == 1:
-            rec["cpu_baseline"] = cpu_baseline(data, args.block_size, chain, args.cpu_seconds)
+            rec["cpu_baseline"] = cpu_baseline(data, bs, chain, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

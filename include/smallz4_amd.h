@@ -43,9 +43,18 @@ const char* sz4_version(void);
 
 /* Create a compression context bound to HIP device `device`.  Scratch space is
  * allocated lazily and grown on demand; `reserve_bytes` pre-sizes it for that
- * much input (0 = on first use). */
+ * much input (0 = on first use).  A context serves one call at a time: threads
+ * that compress concurrently use a context each.  Every call makes the
+ * context's device current and restores the caller's current device. */
 int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes);
 void sz4_destroy(sz4_ctx* ctx);
+
+/* Process-wide context pool (thread-safe): sz4_acquire hands out an idle context of `device` (creating
+ * one when all are busy), sz4_release returns it.  Concurrent callers get different contexts, so
+ * calls through the pool are reentrant -- the reference builds a fresh object per call
+ * (smallz4.h:56-64).  Pooled contexts live until the process exits. */
+int sz4_acquire(sz4_ctx** ctx, int device);
+void sz4_release(sz4_ctx* ctx);
 
 /* Worst-case frame size for n input bytes cut into blocks of block_size. */
 uint64_t sz4_bound(uint64_t n, uint32_t block_size);
@@ -76,12 +85,35 @@ int64_t sz4_last_block_sizes(sz4_ctx* ctx, uint32_t* sizes, uint64_t max_blocks)
  * smallz4::lz4(getBytes, sendBytes, maxChainLength, dictionary, useLegacyFormat)
  * (reference smallz4.h:47-64): 4 MiB dependent blocks (8 MiB independent
  * blocks in legacy format), optional dictionary, identical output bytes.
- * Host buffers; the device does all compression work. */
+ * Host buffers; the device does all compression work, chunk by chunk as in
+ * sz4_lz4_stream (fixed device footprint). */
 int sz4_lz4(sz4_ctx* ctx, const void* in, uint64_t n, uint32_t max_chain, const void* dict,
             uint64_t dict_len, int legacy, void* out, uint64_t out_cap, uint64_t* out_size);
 
 /* Worst-case size of sz4_lz4's output. */
 uint64_t sz4_lz4_bound(uint64_t n, int legacy);
+
+/* The reference's callback types (smallz4.h:41-44): read up to numBytes into data (0 = end of
+ * input); write numBytes from data. */
+typedef size_t (*sz4_get_bytes)(void* data, size_t numBytes, void* userPtr);
+typedef void (*sz4_send_bytes)(const void* data, size_t numBytes, void* userPtr);
+
+/* smallz4::lz4(getBytes, sendBytes, maxChainLength, dictionary, useLegacyFormat, userPtr)
+ * (reference smallz4.h:47-64, 476-813) in bounded memory: the input is pulled through get_bytes
+ * (64 KiB per call, as the reference's BufferSize) and compressed in chunks of whole 4 MiB blocks
+ * (8 MiB legacy) -- sz4_set_stream_chunk bytes per chunk, 64 MiB by default -- each chunk carrying
+ * the previous one's last 64 KiB and chain state, so the output is byte-identical to one pass over
+ * the whole input and the device footprint does not grow with the input.  send_bytes receives the
+ * header, then per block four 1-byte calls for the size word followed by the payload, then the end
+ * mark: the reference's call pattern (smallz4.h:478-496, 770-780, 807-812).  Both callbacks run on
+ * the calling thread; the GPU compresses chunk i while chunk i+1 is read and chunk i-1 is sent.
+ * A context serves one call at a time (use one context per thread). */
+int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_bytes, uint32_t max_chain,
+                   const void* dict, uint64_t dict_len, int legacy, void* user);
+
+/* Input bytes per chunk of the stream paths (sz4_lz4_stream, sz4_lz4; sz4_unlz4_stream queues half
+ * as many frame bytes); rounded down to whole blocks, at least one.  0 restores the 64 MiB default. */
+void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured
  * with HIP events on the call's stream.  stage_ms[0..n) receives
@@ -118,6 +150,22 @@ int sz4_unlz4(sz4_ctx* ctx, const void* frame, uint64_t frame_len, const void* d
  * returns after the stream has finished. */
 int sz4_unlz4_device(sz4_ctx* ctx, const void* d_frame, uint64_t frame_len, const void* d_dict,
                      uint64_t dict_len, void* d_out, uint64_t out_cap, uint64_t* out_size, void* stream);
+
+/* The reference decoder's callback types (smallz4cat.c:62-65). */
+typedef unsigned char (*sz4_get_byte)(void* userPtr);
+typedef void (*sz4_send_out)(const unsigned char* data, unsigned int numBytes, void* userPtr);
+
+/* unlz4_userPtr(getByte, sendBytes, dictionary, userPtr) (smallz4cat.c:112-360) in bounded memory:
+ * get_byte is called where the reference calls it on a valid frame (header, size words, payloads,
+ * checksums; a legacy frame ends after its first block that decodes to less than 8 MiB); blocks are
+ * decoded on the GPU a chunk at a time with the last 64 KiB of output as history, and send_bytes
+ * receives the output in 64 KiB pieces followed by the remainder (the reference's flush points).
+ * dict: the dictionary's bytes (its last 64 KiB are used) or NULL. */
+int sz4_unlz4_stream(sz4_ctx* ctx, sz4_get_byte get_byte, sz4_send_out send_bytes, const void* dict, uint64_t dict_len,
+                     void* user);
+
+/* Device memory (bytes) the context holds: its grow-only scratch, staging and output buffers. */
+uint64_t sz4_device_bytes(sz4_ctx* ctx);
 
 /* Last error message of the context ("" if none). */
 const char* sz4_last_error(sz4_ctx* ctx);

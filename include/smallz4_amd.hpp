@@ -11,14 +11,17 @@
 // sendBytes receives the header, then per block four 1-byte calls for the size word followed
 // by the payload, then the 4-byte end mark (smallz4.h:478-496, 770-780, 809-813).
 //
-// Differences: compression happens on the GPU after the whole input has been read (the
-// reference interleaves reading and compressing 4 MiB at a time); errors from the device are
-// reported as std::runtime_error (the reference has no error path).
+// Memory is bounded as in the reference: the input is compressed in chunks of whole 4 MiB blocks
+// (sz4_lz4_stream), so any input length runs in a fixed device and host footprint.  Calls are
+// reentrant: each call borrows its own context from the library's pool (sz4_acquire), as the
+// reference builds a fresh object per call (smallz4.h:56-64).
+//
+// Differences: errors from the device are reported as std::runtime_error (the reference has no
+// error path); SMALLZ4_AMD_DEVICE=<n> selects the GPU (default 0).
 #pragma once
 
 #include <cstdint>
 #include <cstdlib>
-#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -52,52 +55,28 @@ public:
   static void lz4(GET_BYTES getBytes, SEND_BYTES sendBytes, unsigned short maxChainLength,
                   const std::vector<unsigned char>& dictionary, bool useLegacyFormat = false, void* userPtr = NULL)
   {
-    std::vector<unsigned char> input;
-    std::vector<unsigned char> chunk(64 * 1024);
-    for (;;) {
-      size_t got = getBytes(chunk.data(), chunk.size(), userPtr);
-      if (got == 0) break;
-      input.insert(input.end(), chunk.begin(), chunk.begin() + got);
-    }
-    std::vector<unsigned char> frame(sz4_lz4_bound(input.size(), useLegacyFormat ? 1 : 0));
-    uint64_t size = 0;
-    int rc = sz4_lz4(context(), input.data(), input.size(), maxChainLength, dictionary.empty() ? NULL : dictionary.data(),
-                     dictionary.size(), useLegacyFormat ? 1 : 0, frame.data(), frame.size(), &size);
-    if (rc != SZ4_OK) throw std::runtime_error(std::string("smallz4_amd: ") + sz4_last_error(context()));
-    replay(frame.data(), size, useLegacyFormat, sendBytes, userPtr);
+    Lease ctx;
+    const int rc = sz4_lz4_stream(ctx.c, getBytes, sendBytes, maxChainLength,
+                                  dictionary.empty() ? NULL : dictionary.data(), dictionary.size(),
+                                  useLegacyFormat ? 1 : 0, userPtr);
+    if (rc != SZ4_OK) throw std::runtime_error(std::string("smallz4_amd: ") + sz4_last_error(ctx.c));
   }
 
   /// version string (smallz4.h:67-70)
   static const char* getVersion() { return sz4_version(); }
 
 private:
-  static sz4_ctx* context()
+  // a context of the library's pool for the duration of one call
+  struct Lease
   {
-    static sz4_ctx* ctx = NULL;
-    if (!ctx) {
+    sz4_ctx* c;
+    Lease() : c(NULL)
+    {
       const char* dev = std::getenv("SMALLZ4_AMD_DEVICE");
-      if (sz4_create(&ctx, dev ? std::atoi(dev) : 0, 0) != SZ4_OK)
-        throw std::runtime_error("smallz4_amd: no usable HIP device");
+      if (sz4_acquire(&c, dev ? std::atoi(dev) : 0) != SZ4_OK) throw std::runtime_error("smallz4_amd: no usable HIP device");
     }
-    return ctx;
-  }
-
-  // hand the frame to sendBytes in the reference's call pattern
-  static void replay(const unsigned char* f, uint64_t n, bool legacy, SEND_BYTES sendBytes, void* userPtr)
-  {
-    uint64_t hdr = legacy ? 4 : 7;
-    sendBytes(f, hdr, userPtr);
-    uint64_t pos = hdr;
-    const uint64_t tail = legacy ? 0 : 4;
-    while (pos + tail < n) {
-      uint32_t word = 0;
-      std::memcpy(&word, f + pos, 4);
-      for (int k = 0; k < 4; k++) sendBytes(f + pos + k, 1, userPtr);
-      pos += 4;
-      const uint32_t bytes = word & 0x7FFFFFFFu;
-      sendBytes(f + pos, bytes, userPtr);  // the reference sends the payload even when empty
-      pos += bytes;
-    }
-    if (!legacy) sendBytes(f + pos, 4, userPtr);
-  }
+    ~Lease() { sz4_release(c); }
+    Lease(const Lease&);
+    Lease& operator=(const Lease&);
+  };
 };

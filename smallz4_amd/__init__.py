@@ -84,6 +84,40 @@ class Compressor:
         self._check(rc, "sz4_lz4")
         return out.raw[:size.value]
 
+    def lz4_stream(self, read, write, max_chain_length: int = MaxChainLength, dictionary: bytes = b"",
+                   use_legacy_format: bool = False) -> None:
+        """smallz4::lz4 over callbacks (sz4_lz4_stream): read(n) -> bytes (b"" at the end), write(bytes).
+        Bounded memory: the input is compressed chunk by chunk (set_stream_chunk)."""
+        err = []
+
+        def get(data, n, _user):
+            try:
+                b = read(n)
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the call
+                err.append(e)
+                return 0
+            if b:
+                ctypes.memmove(data, b, len(b))
+            return len(b)
+
+        def send(data, n, _user):
+            try:
+                write(ctypes.string_at(data, n) if n else b"")
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+
+        g, s = _native.GET_BYTES(get), _native.SEND_BYTES(send)
+        dic = bytes(dictionary)
+        rc = self._lib.sz4_lz4_stream(self._h, g, s, int(max_chain_length), dic if dic else None, len(dic),
+                                      int(use_legacy_format), None)
+        if err:
+            raise err[0]
+        self._check(rc, "sz4_lz4_stream")
+
+    def set_stream_chunk(self, nbytes: int):
+        """Input bytes per chunk of the stream paths (whole blocks; 0 = default 64 MiB)."""
+        self._lib.sz4_set_stream_chunk(self._h, int(nbytes))
+
     # -- data-parallel entry point --------------------------------------------------------------
     def compress_blocks_device(self, d_in: int, n: int, d_out: int, out_cap: int, block_size: int = 65536,
                                max_chain_length: int = MaxChainLength, header: str = "smallz4",
@@ -132,6 +166,31 @@ class Compressor:
         self._check(rc, "sz4_unlz4")
         return out.raw[:size.value]
 
+    def unlz4_stream(self, read_byte, write, dictionary: bytes = b"") -> None:
+        """smallz4cat's unlz4_userPtr over callbacks (sz4_unlz4_stream): read_byte() -> int,
+        write(bytes) -- called with 64 KiB pieces and the remainder, as the reference flushes."""
+        err = []
+
+        def get(_user):
+            try:
+                return read_byte()
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+                return 0
+
+        def send(data, n, _user):
+            try:
+                write(ctypes.string_at(data, n) if n else b"")
+            except BaseException as e:  # noqa: BLE001
+                err.append(e)
+
+        g, s = _native.GET_BYTE(get), _native.SEND_OUT(send)
+        dic = bytes(dictionary)
+        rc = self._lib.sz4_unlz4_stream(self._h, g, s, dic if dic else None, len(dic), None)
+        if err:
+            raise err[0]
+        self._check(rc, "sz4_unlz4_stream")
+
     def unlz4_device(self, d_frame: int, n: int, d_out: int, out_cap: int, d_dict: int = 0, dict_len: int = 0,
                      stream: int = 0) -> int:
         """Device pointers in, decoded size out (see sz4_unlz4_device); raises when out_cap is too small."""
@@ -157,6 +216,10 @@ class Compressor:
         ds = np.zeros(n, dtype=np.uint16)
         self._check(self._lib.sz4_debug_matches(self._h, ln.ctypes.data, ds.ctypes.data, n), "sz4_debug_matches")
         return ln, ds
+
+    def device_bytes(self) -> int:
+        """Device memory held by this context (scratch, staging, output buffers)."""
+        return int(self._lib.sz4_device_bytes(self._h))
 
     def set_timing(self, on: bool):
         self._lib.sz4_set_timing(self._h, int(on))

@@ -21,21 +21,32 @@ SZ4_HEADER_NONE = 2
 
 # every symbol include/smallz4_amd.h declares, with its ctypes signature
 _u64, _u32, _i32, _vp = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p
+# the reference's callback types (smallz4.h:41-44, smallz4cat.c:62-65)
+GET_BYTES = ctypes.CFUNCTYPE(ctypes.c_size_t, _vp, ctypes.c_size_t, _vp)
+SEND_BYTES = ctypes.CFUNCTYPE(None, _vp, ctypes.c_size_t, _vp)
+GET_BYTE = ctypes.CFUNCTYPE(ctypes.c_ubyte, _vp)
+SEND_OUT = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_ubyte), ctypes.c_uint, _vp)
 SIGNATURES = {
     "sz4_version": (ctypes.c_char_p, []),
     "sz4_create": (_i32, [ctypes.POINTER(_vp), _i32, _u64]),
     "sz4_destroy": (None, [_vp]),
+    "sz4_acquire": (_i32, [ctypes.POINTER(_vp), _i32]),
+    "sz4_release": (None, [_vp]),
     "sz4_bound": (_u64, [_u64, _u32]),
     "sz4_compress_blocks_device": (_i32, [_vp, _vp, _u64, _u32, _u32, _i32, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     "sz4_last_block_sizes": (ctypes.c_int64, [_vp, ctypes.POINTER(_u32), _u64]),
     "sz4_lz4": (_i32, [_vp, _vp, _u64, _u32, _vp, _u64, _i32, _vp, _u64, ctypes.POINTER(_u64)]),
     "sz4_lz4_bound": (_u64, [_u64, _i32]),
+    "sz4_lz4_stream": (_i32, [_vp, GET_BYTES, SEND_BYTES, _u32, _vp, _u64, _i32, _vp]),
+    "sz4_set_stream_chunk": (None, [_vp, _u64]),
+    "sz4_unlz4_stream": (_i32, [_vp, GET_BYTE, SEND_OUT, _vp, _u64, _vp]),
     "sz4_last_stage_ms": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _i32]),
     "sz4_set_timing": (None, [_vp, _i32]),
     "sz4_debug_stop_after": (None, [_vp, _i32]),
     "sz4_debug_matches": (_i32, [_vp, _vp, _vp, _u64]),
     "sz4_unlz4": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
     "sz4_unlz4_device": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
+    "sz4_device_bytes": (_u64, [_vp]),
     "sz4_last_error": (ctypes.c_char_p, [_vp]),
 }
 

@@ -14,9 +14,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/smallz4_amd.h"
@@ -57,6 +59,45 @@ struct DevBuf {
   T* as() const { return static_cast<T*>(p); }
 };
 
+// pinned host memory (the stream path's chunk buffers), grow-only
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes)
+  {
+    if (bytes <= cap) return hipSuccess;
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e == hipSuccess) cap = bytes;
+    return e;
+  }
+  void release()
+  {
+    if (p) hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// makes the context's device current for the duration of a call and restores the caller's
+struct DeviceGuard {
+  int saved = -1;
+  explicit DeviceGuard(int device)
+  {
+    if (hipGetDevice(&saved) != hipSuccess) saved = -1;
+    if (saved != device) hipSetDevice(device);
+  }
+  ~DeviceGuard()
+  {
+    int now = -1;
+    if (saved >= 0 && hipGetDevice(&now) == hipSuccess && now != saved) hipSetDevice(saved);
+  }
+};
+
 uint32_t xxh32_small(const uint8_t* d, size_t n)
 {
   const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P5 = 374761393u;
@@ -88,7 +129,15 @@ struct sz4_ctx {
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
-  DevBuf dictLast, dictPrevH;  // dictionary mode: the reference's hash table and hash chain
+  DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
+  DevBuf chunkOut;             // stream path: one chunk's blocks
+  HostBuf hostIn[2], hostOut[2];
+  uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
+  // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
+  // (ghost slot nblocks of iv/ivCount, B.prev of the first block) and dictionary-mode state
+  std::vector<Interval> ghostIv;
+  bool ghost = false;
+  uint32_t dictCont = 0, dictShift = 0, dictLow0 = 0;
   DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut;  // decoder (sz4_unlz4*)
   std::vector<UnBlock> hUn;
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
@@ -105,6 +154,19 @@ struct sz4_ctx {
   uint64_t planN = ~0ull;
   uint32_t planBS = 0;
   std::vector<uint32_t> hostBytes;
+
+  hipStream_t stream = nullptr;  // the stream path's own stream
+  bool pooled = false;           // handed out by sz4_acquire
+  std::mutex* poolMu = nullptr;
+  std::vector<sz4_ctx*>* poolIdle = nullptr;
+
+  std::vector<DevBuf*> all_buffers()
+  {
+    return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
+            &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &dictLast, &dictPrevH, &dictPrevX, &chunkOut,
+            &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut};
+  }
 
   int fail(int code, const char* what, hipError_t e = hipSuccess)
   {
@@ -192,8 +254,8 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
   hipError_t e = hipSuccess;
   if ((e = c->blocks.reserve(nb * sizeof(Block) + 64)) ||
       (e = c->segs.reserve(c->hSegs.size() * sizeof(Segment) + 64)) ||
-      (e = c->iv.reserve(nb * kMaxIv * sizeof(Interval) + 64)) ||
-      (e = c->ivCount.reserve(nb * 4 + 64)) ||
+      (e = c->iv.reserve((nb + 1) * kMaxIv * sizeof(Interval) + 64)) ||
+      (e = c->ivCount.reserve((nb + 1) * 4 + 64)) ||
       (e = c->elemA.reserve(c->elemTotal * sizeof(uint2) + 64)) ||
       (e = c->elemB.reserve(c->elemTotal * sizeof(uint2) + 64)) ||
       (e = c->rank.reserve(c->rankTotal * 4 + 64)) ||
@@ -240,6 +302,12 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
       (e = hipMemcpyAsync(c->walkSegs.p, c->hWalk.data(), c->hWalk.size() * sizeof(uint2), hipMemcpyHostToDevice, s)) ||
       (e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
     return c->fail(SZ4_E_DEVICE, "upload plan", e);
+  // ghost slot nb: the previous chunk's last block (only its intervals are read, through B.prev)
+  const uint32_t ghostN = c->ghost ? (uint32_t)c->ghostIv.size() : 0u;
+  if ((ghostN && (e = hipMemcpyAsync(c->iv.as<Interval>() + (uint64_t)nb * kMaxIv, c->ghostIv.data(),
+                                     ghostN * sizeof(Interval), hipMemcpyHostToDevice, s))) ||
+      (e = hipMemcpyAsync(c->ivCount.as<uint32_t>() + nb, &ghostN, 4, hipMemcpyHostToDevice, s)))
+    return c->fail(SZ4_E_DEVICE, "upload intervals", e);
   const uint32_t ns = (uint32_t)c->hSegs.size();
   Block* dB = c->blocks.as<Block>();
   Segment* dS = c->segs.as<Segment>();
@@ -251,11 +319,12 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   mark(c, 1, s);
   if (c->dictBack >= 0 && maxChain > 0) {
     // dictionary mode: the reference's sequential match loop (k_dict_matches), then the usual parse
-    if ((e = c->dictLast.reserve(sizeof(uint32_t) << 20)) || (e = c->dictPrevH.reserve(2 * 65536)))
+    if ((e = c->dictLast.reserve(sizeof(uint32_t) << 20)) || (e = c->dictPrevH.reserve(2 * 65536)) ||
+        (e = c->dictPrevX.reserve(2 * 65536)))
       return c->fail(SZ4_E_NOMEM, "dictionary tables", e);
     launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
-                c->dictPrevH.as<uint16_t>(), c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(),
-                c->longFlag.as<uint32_t>(), s);
+                c->dictPrevH.as<uint16_t>(), c->dictPrevX.as<uint16_t>(), c->dictCont, c->dictShift, c->dictLow0,
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s);
     mark(c, 2, s);
     mark(c, 3, s);
     mark(c, 4, s);
@@ -308,7 +377,8 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   // the parse's reach array is free by now: it holds each block's concatenated match positions
   launch_emit(in, dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), maxChain, chosen, c->mdist.as<uint16_t>(), 0,
               c->walkSlots.as<uint32_t>(), c->walkState.as<uint4>(), c->reach.as<uint32_t>(), c->tokens.as<Token>(),
-              c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen, s);
+              c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen,
+              c->status.as<int>(), s);
   mark(c, 6, s);
   if ((e = hipGetLastError())) return c->fail(SZ4_E_DEVICE, "kernel launch", e);
 
@@ -317,7 +387,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if ((e = hipMemcpyAsync(&total, c->offsets.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s)) ||
       (e = hipMemcpyAsync(&status, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
     return c->fail(SZ4_E_DEVICE, "pipeline", e);
-  (void)status;
+  if (status & kStInvariant) return c->fail(SZ4_E_DEVICE, "device invariant failed (walk slots / token capacity)");
   const uint64_t size = hdrLen + total + (endMark ? 4 : 0);
   if (size > outCap) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
   if (hdrLen && (e = hipMemcpyAsync(out, hdr, hdrLen, hipMemcpyHostToDevice, s)))
@@ -397,6 +467,332 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
   return SZ4_OK;
 }
 
+
+// ---- stream path: smallz4::lz4 over GET_BYTES / SEND_BYTES in bounded memory --------------------
+// The input is compressed in chunks of whole blocks (4 MiB, legacy 8 MiB; c->streamChunk bytes per
+// chunk).  A chunk is staged as [carried bytes | new bytes]: the carried bytes are the previous
+// chunk's last 64..128 KiB (the reference keeps the last MaxDistance bytes, smallz4.h:798-805), so
+// the chunk's first block sees exactly the window the reference's does.  The state a block takes
+// from its predecessor -- the lookback cut (smallz4.h:614-624) and the positions the same-letter
+// shortcut left out of the chains -- comes along as the previous block's final intervals in the
+// ghost slot; dictionary mode carries the reference's hash table and chains.  The device footprint
+// is fixed by the chunk size, whatever the input length.  While the GPU compresses chunk i on a
+// worker thread, the caller's thread hands chunk i-1's blocks to sendBytes and pulls chunk i+1
+// through getBytes (both callbacks always run on the caller's thread).
+constexpr uint64_t kCarryMax = 2 * 65536;
+
+struct MemSource {
+  const uint8_t* p;
+  uint64_t n, at;
+};
+struct MemSink {
+  uint8_t* p;
+  uint64_t cap, n;
+};
+size_t mem_get(void* data, size_t want, void* user)
+{
+  MemSource* m = static_cast<MemSource*>(user);
+  const uint64_t k = std::min<uint64_t>(want, m->n - m->at);
+  if (k) memcpy(data, m->p + m->at, k);
+  m->at += k;
+  return (size_t)k;
+}
+void mem_send(const void* data, size_t n, void* user)
+{
+  MemSink* m = static_cast<MemSink*>(user);
+  if (n && m->n + n <= m->cap) memcpy(m->p + m->n, data, n);
+  m->n += n;
+}
+
+struct ChunkJob {
+  const uint8_t* host;  // pinned: the chunk's new bytes
+  uint64_t pre, n;      // carried bytes already staged, new bytes
+  bool first;           // the stream's first chunk
+  bool more;            // another chunk follows: prepare the carry
+  uint8_t* out;         // pinned: the chunk's blocks
+  uint64_t outSize;
+  uint64_t nextPre;
+  int rc;
+};
+
+// compresses one chunk (worker thread); on success the carry for the next chunk is in place
+int compress_chunk(sz4_ctx* c, uint32_t maxChain, int legacy, bool dictMode, ChunkJob& j)
+{
+  DeviceGuard guard(c->device);
+  hipStream_t s = c->stream;
+  const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
+  c->hBlocks.clear();
+  for (uint64_t st = 0; st < j.n; st += bs) {
+    Block B{};
+    B.start = j.pre + st;
+    B.end = j.pre + std::min(st + bs, j.n);
+    if (legacy || (st == 0 && j.first)) {
+      B.low = B.start;
+      B.cut = kNone;
+      B.prev = kNoBlock;
+    } else {
+      B.low = B.start - kWindow;
+      B.cut = B.start - kTailNoMatch;  // re-inserted by the lookback of the next block
+      B.prev = st == 0 ? kNoBlock - 1 : (uint32_t)c->hBlocks.size() - 1;  // first: the ghost slot, below
+    }
+    B.flags = legacy ? kBlkLegacy : 0;
+    c->hBlocks.push_back(B);
+  }
+  const uint32_t nb = (uint32_t)c->hBlocks.size();
+  if (c->hBlocks[0].prev == kNoBlock - 1) c->hBlocks[0].prev = nb;
+  c->ghost = !legacy && !j.first && !dictMode;
+  finish_plan(c);
+  c->planN = ~0ull;  // invalidate the independent-block plan cache
+  if (int r = reserve_all(c, j.pre + j.n + kPad)) return r;
+  hipError_t e;
+  const uint64_t cap = sz4_lz4_bound(j.n, legacy);
+  if ((e = c->chunkOut.reserve(cap))) return c->fail(SZ4_E_NOMEM, "chunk output", e);
+  uint8_t* staged = c->staged.as<uint8_t>();
+  if ((e = hipMemcpyAsync(staged + j.pre, j.host, j.n, hipMemcpyHostToDevice, s)) ||
+      (e = hipMemsetAsync(staged + j.pre + j.n, 0, kPad, s)))
+    return c->fail(SZ4_E_DEVICE, "upload", e);
+  uint64_t size = 0;
+  if (int r = run_pipeline(c, maxChain, nullptr, 0, false, c->chunkOut.as<uint8_t>(), cap, &size, s)) return r;
+  if ((e = hipMemcpyAsync(j.out, c->chunkOut.p, size, hipMemcpyDeviceToHost, s))) return c->fail(SZ4_E_DEVICE, "download", e);
+  j.outSize = size;
+  if (j.more) {
+    // carry: the last (pre + n - shift) bytes, shift a multiple of 65536 so that dictionary mode's
+    // absolute chain slots (pos & 65535) stay put; at least 65536 bytes precede the next chunk
+    const uint64_t end = j.pre + j.n;
+    const uint64_t shift = (end - 65536) / 65536 * 65536;
+    j.nextPre = end - shift;
+    if (!legacy && !dictMode) {
+      // the last block's final shortcut intervals become the next chunk's ghost slot
+      uint32_t cnt = 0;
+      if ((e = hipMemcpyAsync(&cnt, c->ivCount.as<uint32_t>() + (nb - 1), 4, hipMemcpyDeviceToHost, s)) ||
+          (e = hipStreamSynchronize(s)))
+        return c->fail(SZ4_E_DEVICE, "intervals", e);
+      std::vector<Interval> iv(cnt);
+      if (cnt && ((e = hipMemcpyAsync(iv.data(), c->iv.as<Interval>() + (uint64_t)(nb - 1) * kMaxIv, cnt * sizeof(Interval),
+                                      hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))))
+        return c->fail(SZ4_E_DEVICE, "intervals", e);
+      c->ghostIv.clear();
+      for (Interval x : iv) {
+        if (x.hi <= shift) continue;
+        x.lo = std::max(x.lo, shift) - shift;
+        x.hi -= shift;
+        x.a = x.a >= shift ? x.a - shift : 0;
+        c->ghostIv.push_back(x);
+      }
+    }
+    if (dictMode) {
+      c->dictCont = legacy ? 0u : 1u;
+      c->dictShift = (uint32_t)shift;
+      c->dictLow0 = (uint32_t)(j.nextPre - kWindow);
+    }
+    // the source [shift, end) and the destination [0, end - shift) do not overlap: end - shift <= 2 * 65536 <= shift
+    if ((e = hipMemcpyAsync(staged, staged + shift, j.nextPre, hipMemcpyDeviceToDevice, s))) return c->fail(SZ4_E_DEVICE, "carry", e);
+  }
+  if ((e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "chunk", e);
+  return SZ4_OK;
+}
+
+// the reference's output call pattern for a run of blocks: four 1-byte calls for the size word, then
+// the payload, also when it is empty (smallz4.h:770-780)
+void send_blocks(const uint8_t* f, uint64_t n, sz4_send_bytes send, void* user)
+{
+  uint64_t pos = 0;
+  while (pos + 4 <= n) {
+    uint32_t word = 0;
+    memcpy(&word, f + pos, 4);
+    for (int k = 0; k < 4; k++) send(f + pos + k, 1, user);
+    pos += 4;
+    const uint32_t bytes = word & 0x7FFFFFFFu;
+    send(f + pos, bytes, user);
+    pos += bytes;
+  }
+}
+
+// reads up to `want` bytes through getBytes, 64 KiB per call (the reference's BufferSize); *eof is
+// set once getBytes has returned 0
+uint64_t pull(sz4_get_bytes get, void* user, uint8_t* dst, uint64_t want, bool* eof)
+{
+  uint64_t got = 0;
+  while (got < want && !*eof) {
+    const size_t k = get(dst + got, (size_t)std::min<uint64_t>(65536, want - got), user);
+    if (k == 0) *eof = true;
+    got += k;
+  }
+  return got;
+}
+
+int stream_compress(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t maxChain, const uint8_t* dict,
+                    uint64_t dictLen, int legacy, void* user, void* sinkUser = nullptr)
+{
+  void* out = sinkUser ? sinkUser : user;
+  hipError_t e;
+  if (!c->stream && (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)))
+    return c->fail(SZ4_E_DEVICE, "stream", e);
+  const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
+  const uint64_t chunk = std::max<uint64_t>(bs, c->streamChunk / bs * bs);
+  const bool dictMode = dictLen != 0;
+  // header (smallz4.h:478-496)
+  const uint8_t hm[7] = {0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF};
+  const uint8_t hl[4] = {0x02, 0x21, 0x4C, 0x18};
+  send(legacy ? hl : hm, legacy ? 4 : 7, out);
+  if ((e = c->hostIn[0].reserve(chunk)) || (e = c->hostIn[1].reserve(chunk)) ||
+      (e = c->hostOut[0].reserve(sz4_lz4_bound(chunk, legacy))) || (e = c->hostOut[1].reserve(sz4_lz4_bound(chunk, legacy))))
+    return c->fail(SZ4_E_NOMEM, "pinned host buffers", e);
+  // fixed device footprint: the staged buffer is sized once for the largest chunk (the carry lives in it)
+  if ((e = c->staged.reserve(kCarryMax + chunk + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
+  bool eof = false;
+  uint64_t n = pull(get, user, c->hostIn[0].as<uint8_t>(), chunk, &eof);
+  // dictionary: the staged stream starts with the reference's data buffer, a 65535-byte prefix (the
+  // dictionary's last bytes, zero-padded in front) (smallz4.h:554-571)
+  uint64_t pre = 0;
+  c->dictBack = dictMode ? (int64_t)std::min<uint64_t>(dictLen, kWindow) : -1;
+  c->dictLegacy = legacy;
+  c->dictCont = 0;
+  c->ghost = false;
+  if (dictMode && n) {
+    pre = kWindow;
+    std::vector<uint8_t> prefix(pre, 0);
+    const uint64_t k = std::min<uint64_t>(dictLen, pre);
+    memcpy(prefix.data() + pre - k, dict + dictLen - k, k);
+    if ((e = hipMemcpy(c->staged.p, prefix.data(), pre, hipMemcpyHostToDevice))) return c->fail(SZ4_E_DEVICE, "upload", e);
+  }
+  ChunkJob prevJob{};
+  bool havePrev = false;
+  for (uint32_t i = 0; n; i++) {
+    ChunkJob j{};
+    j.host = c->hostIn[i & 1].as<uint8_t>();
+    j.pre = pre;
+    j.n = n;
+    j.first = i == 0;
+    j.more = n == chunk && !eof;
+    j.out = c->hostOut[i & 1].as<uint8_t>();
+    j.rc = SZ4_OK;
+    std::thread worker([&]() { j.rc = compress_chunk(c, maxChain, legacy, dictMode, j); });
+    // meanwhile, on the caller's thread: the previous chunk's blocks out, the next chunk's bytes in
+    if (havePrev) send_blocks(prevJob.out, prevJob.outSize, send, out);
+    const uint64_t next = j.more ? pull(get, user, c->hostIn[(i + 1) & 1].as<uint8_t>(), chunk, &eof) : 0;
+    worker.join();
+    if (j.rc != SZ4_OK) return j.rc;
+    prevJob = j;
+    havePrev = true;
+    pre = j.nextPre;
+    n = next;
+  }
+  if (havePrev) send_blocks(prevJob.out, prevJob.outSize, send, out);
+  if (!legacy) {
+    static const uint8_t zero[4] = {0, 0, 0, 0};
+    send(zero, 4, out);  // end mark (smallz4.h:807-812)
+  }
+  return SZ4_OK;
+}
+
+// ---- decoder stream path: unlz4_userPtr over GET_BYTE / SEND_BYTES in bounded memory -----------
+// getByte is called exactly where the reference calls it on a valid frame (header, size words,
+// payloads, checksums; a legacy frame ends after its first block that decodes to less than 8 MiB,
+// smallz4cat.c:325-327).  Blocks are pulled until about c->streamChunk / 2 frame bytes are queued,
+// rewrapped as a plain frame (smallz4's header, the blocks, an end mark; checksums dropped) and
+// decoded on the GPU with the last 64 KiB of output (at first the dictionary's) as its history.
+// sendBytes receives the output in 64 KiB pieces and the remainder at the end -- the reference's
+// flush points (smallz4cat.c:249-253, 358-359).
+uint64_t legacy_block_length(const uint8_t* p, uint64_t len)
+{
+  uint64_t r = 0, w = 0;
+  while (r < len) {
+    const uint8_t tok = p[r++];
+    uint64_t lits = tok >> 4, ml = 4 + (tok & 15);
+    uint8_t x;
+    if (lits == 15) do { if (r >= len) return w; x = p[r++]; lits += x; } while (x == 255);
+    r += lits;
+    w += lits;
+    if (r >= len) break;
+    r += 2;
+    if (ml == 19) do { if (r >= len) return w; x = p[r++]; ml += x; } while (x == 255);
+    w += ml;
+  }
+  return w;
+}
+
+int stream_decompress(sz4_ctx* c, sz4_get_byte get, sz4_send_out send, const uint8_t* dict, uint64_t dictLen, void* user)
+{
+  uint32_t sig = 0;
+  for (int k = 0; k < 4; k++) sig |= (uint32_t)get(user) << (8 * k);
+  const bool modern = sig == 0x184D2204u, legacy = sig == 0x184C2102u;
+  if (!modern && !legacy) return c->fail(SZ4_E_CORRUPT, "invalid signature");
+  bool blockSum = false, contentSum = false;
+  if (modern) {
+    const uint8_t flags = get(user);
+    if ((flags >> 6) != 1) return c->fail(SZ4_E_CORRUPT, "only LZ4 file format version 1 supported");
+    blockSum = (flags & 16) != 0;
+    contentSum = (flags & 4) != 0;
+    int skip = 1 + ((flags & 8) ? 8 : 0) + ((flags & 1) ? 4 : 0) + 1;
+    while (skip--) get(user);
+  }
+  std::vector<uint8_t> hist;  // the last <= 64 KiB before the next chunk's output
+  if (dictLen) hist.assign(dict + (dictLen - std::min<uint64_t>(dictLen, 65536)), dict + dictLen);
+  std::vector<uint8_t> frame, out, pend;  // pend: output not yet flushed (< 64 KiB)
+  const uint8_t hdr[7] = {0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF};
+  const uint64_t budget = std::max<uint64_t>(c->streamChunk / 2, 1u << 20);
+  auto decode = [&]() -> int {
+    if (frame.size() <= 7) return SZ4_OK;
+    for (int k = 0; k < 4; k++) frame.push_back(0);  // end mark
+    uint64_t size = 0;
+    int r = sz4_unlz4(c, frame.data(), frame.size(), hist.empty() ? nullptr : hist.data(), hist.size(), nullptr, 0, &size);
+    if (r == SZ4_E_CAPACITY) {
+      out.resize(size);
+      r = sz4_unlz4(c, frame.data(), frame.size(), hist.empty() ? nullptr : hist.data(), hist.size(), out.data(), size, &size);
+    } else {
+      out.clear();
+    }
+    if (r != SZ4_OK) return r;
+    out.resize(size);
+    // new history: the last 64 KiB of (history, output)
+    if (size >= 65536) {
+      hist.assign(out.end() - 65536, out.end());
+    } else {
+      hist.insert(hist.end(), out.begin(), out.end());
+      if (hist.size() > 65536) hist.erase(hist.begin(), hist.end() - 65536);
+    }
+    // flush in 64 KiB pieces
+    uint64_t at = 0;
+    if (!pend.empty()) {
+      const uint64_t k = std::min<uint64_t>(65536 - pend.size(), size);
+      pend.insert(pend.end(), out.begin(), out.begin() + k);
+      at = k;
+      if (pend.size() == 65536) {
+        send(pend.data(), 65536, user);
+        pend.clear();
+      }
+    }
+    for (; at + 65536 <= size; at += 65536) send(out.data() + at, 65536, user);
+    pend.insert(pend.end(), out.begin() + at, out.begin() + size);
+    frame.assign(hdr, hdr + 7);
+    return SZ4_OK;
+  };
+  frame.assign(hdr, hdr + 7);
+  for (;;) {
+    uint32_t word = 0;
+    for (int k = 0; k < 4; k++) word |= (uint32_t)get(user) << (8 * k);
+    const bool packed = legacy || (word & 0x80000000u) == 0;
+    if (modern) word &= 0x7FFFFFFFu;
+    if (word == 0) break;
+    if (legacy && (word & 0x80000000u)) return c->fail(SZ4_E_CORRUPT, "invalid or truncated LZ4 frame");
+    const uint64_t at = frame.size();
+    frame.resize(at + 4 + word);
+    const uint32_t tagged = word | (packed ? 0u : 0x80000000u);
+    memcpy(frame.data() + at, &tagged, 4);
+    for (uint32_t k = 0; k < word; k++) frame[at + 4 + k] = get(user);
+    if (legacy && packed && legacy_block_length(frame.data() + at + 4, word) < kBlockMaxLegacy) break;
+    if (blockSum)
+      for (int k = 0; k < 4; k++) get(user);
+    if (frame.size() >= budget)
+      if (int r = decode()) return r;
+  }
+  if (contentSum)
+    for (int k = 0; k < 4; k++) get(user);
+  if (int r = decode()) return r;
+  send(pend.data(), (unsigned int)pend.size(), user);
+  return SZ4_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -409,7 +805,7 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   *ctx = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count) return SZ4_E_DEVICE;
-  if (hipSetDevice(device) != hipSuccess) return SZ4_E_DEVICE;
+  DeviceGuard guard(device);
   sz4_ctx* c = new sz4_ctx();
   c->device = device;
   const char* sep = getenv("SZ4_SEPARATE_SORT");
@@ -426,16 +822,44 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
 void sz4_destroy(sz4_ctx* c)
 {
   if (!c) return;
-  hipSetDevice(c->device);
-  for (DevBuf* b : {&c->staged, &c->blocks, &c->segs, &c->iv, &c->ivCount, &c->elemA, &c->elemB, &c->rank, &c->mlen,
-                    &c->mdist, &c->cost, &c->tokens, &c->ntok, &c->blockBytes, &c->offsets, &c->status, &c->dpSegs,
-                    &c->sel, &c->reach, &c->segState, &c->walkSegs, &c->walkSlots, &c->walkState, &c->longFlag,
-                    &c->rmqUp, &c->rmqDown, &c->longBits, &c->segLong, &c->dictLast, &c->dictPrevH, &c->unBlk,
-                    &c->unMeta, &c->unFlags, &c->unFrame, &c->unDict, &c->unOut})
-    b->release();
+  DeviceGuard guard(c->device);
+  for (DevBuf* b : c->all_buffers()) b->release();
+  for (HostBuf* b : {&c->hostIn[0], &c->hostIn[1], &c->hostOut[0], &c->hostOut[1]}) b->release();
+  if (c->stream) hipStreamDestroy(c->stream);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   delete c;
+}
+
+int sz4_acquire(sz4_ctx** ctx, int device)
+{
+  if (!ctx) return SZ4_E_ARG;
+  static std::mutex mu;
+  static std::vector<sz4_ctx*>* idle = new std::vector<sz4_ctx*>();  // never destroyed: contexts outlive exit order
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    for (size_t i = 0; i < idle->size(); i++)
+      if ((*idle)[i]->device == device) {
+        *ctx = (*idle)[i];
+        idle->erase(idle->begin() + (long)i);
+        (*ctx)->pooled = true;
+        return SZ4_OK;
+      }
+  }
+  const int r = sz4_create(ctx, device, 0);
+  if (r == SZ4_OK) {
+    (*ctx)->pooled = true;
+    (*ctx)->poolMu = &mu;
+    (*ctx)->poolIdle = idle;
+  }
+  return r;
+}
+
+void sz4_release(sz4_ctx* c)
+{
+  if (!c || !c->pooled || !c->poolMu) return;
+  std::lock_guard<std::mutex> lock(*c->poolMu);
+  c->poolIdle->push_back(c);
 }
 
 uint64_t sz4_bound(uint64_t n, uint32_t block_size)
@@ -461,7 +885,8 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   c->err.clear();
   // the kernels write the frame in place: refuse a buffer that could be overrun
   if (out_cap < sz4_bound(n, block_size)) return c->fail(SZ4_E_CAPACITY, "out_cap < sz4_bound(n, block_size)");
-  hipSetDevice(c->device);
+  DeviceGuard guard(c->device);
+  c->ghost = false;
   hipStream_t s = (hipStream_t)stream;
   c->dictBack = -1;
   if (c->planN != n || c->planBS != block_size) {
@@ -526,83 +951,36 @@ int64_t sz4_last_block_sizes(sz4_ctx* c, uint32_t* sizes, uint64_t max_blocks)
   return (int64_t)nb;
 }
 
+int sz4_lz4_stream(sz4_ctx* c, sz4_get_bytes get_bytes, sz4_send_bytes send_bytes, uint32_t max_chain, const void* dict,
+                   uint64_t dict_len, int legacy, void* user)
+{
+  if (!c || !get_bytes || !send_bytes || max_chain > 65535 || (dict_len && !dict))
+    return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
+  c->err.clear();
+  DeviceGuard guard(c->device);
+  return stream_compress(c, get_bytes, send_bytes, max_chain, (const uint8_t*)dict, dict_len, legacy, user);
+}
+
 int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const void* dict, uint64_t dict_len, int legacy,
             void* out, uint64_t out_cap, uint64_t* out_size)
 {
   if (!c || !out_size || (!in && n) || !out || max_chain > 65535 || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
   c->err.clear();
-  hipSetDevice(c->device);
-  hipStream_t s = nullptr;
-  // dictionary: the staged stream is the reference's data buffer, a 65535-byte prefix (the dictionary's
-  // last bytes, zero-padded in front) and then the input (smallz4.h:554-571)
-  const uint64_t pre = dict_len ? kWindow : 0;
-  c->dictBack = dict_len ? (int64_t)std::min<uint64_t>(dict_len, kWindow) : -1;
-  c->dictLegacy = legacy;
-  // block structure of smallz4::compress (smallz4.h:541-606, 614-624, 782-805)
-  const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
-  c->hBlocks.clear();
-  for (uint64_t st = 0; st < n; st += bs) {
-    Block B{};
-    B.start = pre + st;
-    B.end = pre + std::min(st + bs, n);
-    const bool first = st == 0;
-    if (legacy || first) {
-      B.low = B.start;
-      B.cut = kNone;
-      B.prev = kNoBlock;
-    } else {
-      B.low = B.start - kWindow;
-      B.cut = B.start - kTailNoMatch;  // re-inserted by the lookback of the next block
-      B.prev = (uint32_t)c->hBlocks.size() - 1;
-    }
-    B.flags = legacy ? kBlkLegacy : 0;
-    c->hBlocks.push_back(B);
-  }
-  finish_plan(c);
-  c->planN = ~0ull;  // invalidate the independent-block plan cache
-  if (int r = reserve_all(c, pre + n + kPad)) return r;
-  hipError_t e;
-  if ((e = c->staged.reserve(pre + n + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
-  DevBuf dout;
-  const uint64_t cap = sz4_lz4_bound(n, legacy);
-  if ((e = dout.reserve(cap))) return c->fail(SZ4_E_NOMEM, "output", e);
-  if (pre) {
-    std::vector<uint8_t> prefix(pre, 0);
-    const uint64_t k = std::min<uint64_t>(dict_len, pre);
-    memcpy(prefix.data() + pre - k, (const uint8_t*)dict + dict_len - k, k);
-    if ((e = hipMemcpy(c->staged.p, prefix.data(), pre, hipMemcpyHostToDevice))) {
-      dout.release();
-      return c->fail(SZ4_E_DEVICE, "upload", e);
-    }
-  }
-  if (n && (e = hipMemcpy(c->staged.as<uint8_t>() + pre, in, n, hipMemcpyHostToDevice))) {
-    dout.release();
-    return c->fail(SZ4_E_DEVICE, "upload", e);
-  }
-  hipMemset(c->staged.as<uint8_t>() + pre + n, 0, kPad);
-  const uint8_t hm[7] = {0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF};
-  const uint8_t hl[4] = {0x02, 0x21, 0x4C, 0x18};
-  uint64_t size = 0;
-  int r;
-  if (n == 0) {
-    size = legacy ? 4 : 11;
-    if (size > out_cap) r = c->fail(SZ4_E_CAPACITY, "output buffer too small");
-    else {
-      memcpy(out, legacy ? hl : hm, legacy ? 4 : 7);
-      if (!legacy) memset((uint8_t*)out + 7, 0, 4);
-      r = SZ4_OK;
-    }
-  } else {
-    r = run_pipeline(c, max_chain, legacy ? hl : hm, legacy ? 4 : 7, !legacy, dout.as<uint8_t>(), cap, &size, s);
-    if (r == SZ4_OK) {
-      if (size > out_cap) r = c->fail(SZ4_E_CAPACITY, "output buffer too small");
-      else if ((e = hipMemcpy(out, dout.p, size, hipMemcpyDeviceToHost))) r = c->fail(SZ4_E_DEVICE, "download", e);
-    }
-  }
-  dout.release();
-  if (r == SZ4_OK) *out_size = size;
-  return r;
+  DeviceGuard guard(c->device);
+  // the stream path over memory: the source hands out 64 KiB pieces, the sink appends
+  MemSource src{(const uint8_t*)in, n, 0};
+  MemSink dst{(uint8_t*)out, out_cap, 0};
+  const int r = stream_compress(c, mem_get, mem_send, max_chain, (const uint8_t*)dict, dict_len, legacy, &src, &dst);
+  if (r != SZ4_OK) return r;
+  if (dst.n > out_cap) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
+  *out_size = dst.n;
+  return SZ4_OK;
+}
+
+void sz4_set_stream_chunk(sz4_ctx* c, uint64_t bytes)
+{
+  if (c) c->streamChunk = bytes ? bytes : (64ull << 20);
 }
 
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)
@@ -641,7 +1019,7 @@ int sz4_unlz4_device(sz4_ctx* c, const void* d_frame, uint64_t frame_len, const 
   if (!c || !out_size || (!d_frame && frame_len) || (dict_len && !d_dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
   c->err.clear();
-  hipSetDevice(c->device);
+  DeviceGuard guard(c->device);
   hipStream_t s = (hipStream_t)stream;
   uint64_t total = 0;
   uint32_t keep = 0;
@@ -660,7 +1038,7 @@ int sz4_unlz4(sz4_ctx* c, const void* frame, uint64_t frame_len, const void* dic
   if (!c || !out_size || (!frame && frame_len) || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
   c->err.clear();
-  hipSetDevice(c->device);
+  DeviceGuard guard(c->device);
   hipError_t e;
   const uint64_t dl = std::min<uint64_t>(dict_len, 65536);
   if ((e = c->unFrame.reserve(frame_len + 64)) || (e = c->unDict.reserve(dl + 64)))
@@ -680,6 +1058,23 @@ int sz4_unlz4(sz4_ctx* c, const void* frame, uint64_t frame_len, const void* dic
     return r;
   if ((e = hipMemcpy(out, c->unOut.p, total, hipMemcpyDeviceToHost))) return c->fail(SZ4_E_DEVICE, "download", e);
   return SZ4_OK;
+}
+
+int sz4_unlz4_stream(sz4_ctx* c, sz4_get_byte get_byte, sz4_send_out send_bytes, const void* dict, uint64_t dict_len,
+                     void* user)
+{
+  if (!c || !get_byte || !send_bytes || (dict_len && !dict)) return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
+  c->err.clear();
+  DeviceGuard guard(c->device);
+  return stream_decompress(c, get_byte, send_bytes, (const uint8_t*)dict, dict_len, user);
+}
+
+uint64_t sz4_device_bytes(sz4_ctx* c)
+{
+  if (!c) return 0;
+  uint64_t t = 0;
+  for (const DevBuf* b : c->all_buffers()) t += b->cap;
+  return t;
 }
 
 const char* sz4_last_error(sz4_ctx* c) { return c ? c->err.c_str() : "no context"; }

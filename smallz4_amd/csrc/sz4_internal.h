@@ -20,6 +20,10 @@ constexpr int kHashBits = 20;
 constexpr uint64_t kNone = ~0ull;
 constexpr int kStages = 6;  // runs, sort, find (sorted pass), find (long pass), parse, assemble
 
+// device status word bits (one int per pipeline run)
+constexpr int kStPrepRound = 2;   // k_prep corrected a shortcut interval: run sort/find/prep again
+constexpr int kStInvariant = 4;   // a capacity invariant of the walk/token kernels failed: the frame is invalid
+
 // one LZ4 block (all positions absolute byte offsets in the staged input)
 struct Block {
   uint64_t start, end;     // [start, end)
@@ -54,7 +58,8 @@ struct Interval {
   uint64_t a;              // the position whose distance-1 match starts the shortcut
   uint64_t La;             // its match length
 };
-// block b owns iv[b * kMaxIv .. b * kMaxIv + ivCount[b])
+// block b owns iv[b * kMaxIv .. b * kMaxIv + ivCount[b]); slot nblocks holds the final intervals of the
+// previous chunk's last block when a stream is compressed in chunks (the first block's B.prev)
 constexpr uint32_t kMaxIv = 136;  // > 8 MiB / 65300
 
 // the optimal parse of one block runs as independent segments of B.dpSize positions (top segment
@@ -101,10 +106,12 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
                  bool ldsWindow, uint32_t hybridLds, bool fuseSort, hipStream_t s);
 // dictionary mode: one wavefront replays the reference's match loop (dictBack = first insertion offset
-// before the first block); last: 2^20 u32 scratch, prevH: 65536 u16 scratch
+// before the first block); last: 2^20 u32, prevH / prevX: 65536 u16 each -- the reference's tables,
+// kept in HBM between the chunks of one stream.  cont: the first block continues the stream of the
+// previous launch, whose staged positions were `shift` (a multiple of 65536) higher; low0 = its dataZero
 void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
-                 uint32_t* last, uint16_t* prevH, uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag,
-                 hipStream_t s);
+                 uint32_t* last, uint16_t* prevH, uint16_t* prevX, uint32_t cont, uint32_t shift, uint32_t low0,
+                 uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, hipStream_t s);
 // k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
 // corrected, run sort/find/prep again
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
@@ -116,7 +123,7 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
                  uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
                  uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
-                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s);
+                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, int* status, hipStream_t s);
 
 // decoder (sz4_unlz4.hip): one block of an LZ4 frame
 struct UnBlock {

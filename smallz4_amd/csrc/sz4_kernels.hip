@@ -2020,7 +2020,8 @@ constexpr uint32_t kNoPos = 0xFFFFFFFFu;
 __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
                                                      uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
                                                      uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
-                                                     uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                     uint16_t* __restrict__ prevXg, uint32_t cont, uint32_t shift,
+                                                     uint32_t low0, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                      uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
 {
   __shared__ uint16_t prevX[65536];
@@ -2032,7 +2033,18 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
     }
     for (uint32_t j = lane; j < (1u << kHashBits); j += 64) last[j] = kNoPos;
   };
-  reset();
+  if (!cont) {
+    reset();
+  } else {
+    // the previous chunk's tables: chain slots are absolute positions mod 65536, unchanged by a shift
+    // that is a multiple of 65536; positions that fall below the carried bytes become "no entry" (the
+    // reference finds them more than MaxDistance away)
+    for (uint32_t j = lane; j < 65536; j += 64) prevX[j] = prevXg[j];
+    for (uint32_t j = lane; j < (1u << kHashBits); j += 64) {
+      const uint32_t v = last[j];
+      last[j] = (v == kNoPos || v < shift) ? kNoPos : v - shift;
+    }
+  }
   for (uint32_t b = 0; b < nblocks; b++) {
     const Block B = blocks[b];
     for (uint64_t i = B.start + lane; i < B.end; i += 64) {
@@ -2046,12 +2058,14 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
   if (lane != 0) return;
 
   const bool greedy = maxChain <= (uint32_t)kGreedyMax, lazy = !greedy && maxChain <= (uint32_t)kLazyMax;
-  uint64_t low = 0;  // reference dataZero
-  bool withDict = true;
+  uint64_t low = cont ? low0 : 0;  // reference dataZero
+  bool withDict = !cont;
   for (uint32_t b = 0; b < nblocks; b++) {
     const Block B = blocks[b];
     const uint64_t start = B.start, size = B.end - B.start, stop = B.end - kTailLiterals;
-    int64_t back = withDict ? -(int64_t)dictBack : -(int64_t)(low < (uint64_t)kTailNoMatch ? low : (uint64_t)kTailNoMatch);
+    // the first block inserts the dictionary; every later one re-inserts the last 12 positions before
+    // it (dataZero > BlockEndNoMatch from the second block on, smallz4.h:612-620)
+    int64_t back = withDict ? -(int64_t)dictBack : -(int64_t)kTailNoMatch;
     if (legacy) back = 0;
     uint64_t skip = 0;
     bool lazyEval = false, rmq = false;
@@ -2143,20 +2157,16 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
       low = B.end - kWindow;  // the reference keeps only the last 64 KiB - 1 (smallz4.h:799-804)
     }
   }
+  for (uint32_t j = 0; j < 65536; j++) prevXg[j] = prevX[j];  // carried to the next chunk
 }
 
 void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
-                 uint32_t* last, uint16_t* prevH, uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag,
-                 hipStream_t s)
+                 uint32_t* last, uint16_t* prevH, uint16_t* prevX, uint32_t cont, uint32_t shift, uint32_t low0,
+                 uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, hipStream_t s)
 {
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute((const void*)k_dict_matches, hipFuncAttributeMaxDynamicSharedMemorySize, 0);
-    attr = true;
-  }
   if (nblocks)
     hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, legacy, last, prevH,
-                       mlen, mdist, sel, longFlag);
+                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag);
 }
 
 // Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut
@@ -2881,7 +2891,8 @@ constexpr int kWalkWaves = 4;  // sub-segments per k_walk workgroup
 __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restrict__ blocks,
                                                           const uint2* __restrict__ walkSegs, uint32_t nwalk,
                                                           const uint32_t* __restrict__ chosen, uint64_t matchBase,
-                                                          uint32_t* __restrict__ slotsAll, uint4* __restrict__ state)
+                                                          uint32_t* __restrict__ slotsAll, uint4* __restrict__ state,
+                                                          int* __restrict__ status)
 {
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t idx = blockIdx.x * kWalkWaves + wave;
@@ -2931,6 +2942,11 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
       viaMatch = false;
       continue;
     }
+    if (m >= kWalkCap) {
+      // a match is at least kMinMatch long, so a sub-segment holds at most kWalkSeg / 4 + 1 of them
+      if (lane == 0) atomicOr(status, kStInvariant);
+      break;
+    }
     if (lane == 0) slots[m] = q;
     m++;
     pos = q + rdlane(wL, q - wbase);
@@ -2945,7 +2961,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
 // speculative matches that survive.
 __global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ chosen,
                                                  uint64_t matchBase, uint32_t* __restrict__ slotsAll,
-                                                 uint4* __restrict__ state)
+                                                 uint4* __restrict__ state, int* __restrict__ status)
 {
   __shared__ uint32_t fix[kWalkCap];
   const Block B = blocks[blockIdx.x];
@@ -2988,6 +3004,10 @@ __global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ block
     while (q < aNext) {
       const uint32_t lq = L[q];
       if (lq > 1u) {
+        if (f >= kWalkCap) {
+          if (lane == 0) atomicOr(status, kStInvariant);
+          break;
+        }
         if (lane == 0) fix[f] = q;
         f++;
         q += lq;
@@ -3166,7 +3186,8 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_seg_tokens(const Block* __re
 // per block: byte offsets of its sub-segments, its encoded size and the stored/compressed decision
 __global__ __launch_bounds__(kAsmThreads) void k_block_bytes(const Block* __restrict__ blocks, uint32_t maxChain,
                                                              uint4* __restrict__ info, const uint2* __restrict__ blockTail,
-                                                             uint32_t* __restrict__ ntokOut, uint32_t* __restrict__ blockBytes)
+                                                             uint32_t* __restrict__ ntokOut, uint32_t* __restrict__ blockBytes,
+                                                             int* __restrict__ status)
 {
   __shared__ uint32_t s_sum[kAsmThreads / 64];
   const Block B = blocks[blockIdx.x];
@@ -3198,6 +3219,8 @@ __global__ __launch_bounds__(kAsmThreads) void k_block_bytes(const Block* __rest
   }
   const bool useEnc = (enc < n && !stored) || legacy;
   const uint32_t bytes = (uint32_t)(useEnc ? enc : n);
+  // a block's tokens fit its Token slots ((n / 2 + 4), one match per >= 4 bytes) and its size word
+  if (tid == 0 && (ntok > n / 2 + 4 || (useEnc ? enc : n) >= 0x7FFFFFFBull)) atomicOr(status, kStInvariant);
   if (tid == 0) {
     ntokOut[blockIdx.x] = useEnc ? ntok : 0u;
     blockBytes[blockIdx.x] = (useEnc ? 0u : 0x80000000u) | (bytes + 4u);
@@ -3337,13 +3360,11 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
   if (!nsegs) return;
   const bool unlimited = maxChain >= 65535u;
   if (ldsWindow) {
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)k_find<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
-      hipFuncSetAttribute((const void*)k_find_sorted<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
-      hipFuncSetAttribute((const void*)k_find_long9<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
-      attr = true;
-    }
+    // dynamic-LDS limits are per function and device: set them on every launch (a host-side call,
+    // no synchronisation) rather than caching them process-wide
+    const void* fn = pass == 1 ? (const void*)k_find_sorted<true>
+                     : unlimited ? (const void*)k_find_long9<true> : (const void*)k_find<true>;
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                          ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank,
@@ -3358,20 +3379,12 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                          compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
   } else {
     if (pass == 1) {
-      static uint32_t attrBytes1 = 0;
-      if (hybridLds > attrBytes1) {
-        hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
-        attrBytes1 = hybridLds;
-      }
+      hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {
-      static uint32_t attrBytes = 0;
-      if (hybridLds > attrBytes) {
-        hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
-        attrBytes = hybridLds;
-      }
+      hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
                            compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen, specDist,
@@ -3411,13 +3424,13 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
                  uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
                  uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,
-                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, hipStream_t s)
+                 uint64_t* offsets, uint8_t* out, uint64_t headerLen, int* status, hipStream_t s)
 {
   if (!nblocks) return;
   if (maxChain > 0 && nwalk) {
     hipLaunchKernelGGL(k_walk, dim3((nwalk + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs,
-                       nwalk, chosen, matchBase, walkSlots, walkState);
-    hipLaunchKernelGGL(k_walk_fix, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState);
+                       nwalk, chosen, matchBase, walkSlots, walkState, status);
+    hipLaunchKernelGGL(k_walk_fix, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState, status);
   }
   // per-sub-segment scratch in posList (the parse's reach array, free by now)
   uint4* info = reinterpret_cast<uint4*>(posList);
@@ -3428,7 +3441,8 @@ void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
     hipLaunchKernelGGL(k_seg_tokens, dim3(segGrid), dim3(64 * kSegWaves), 0, s, blocks, walkSegs, nwalk, chosen, mdist, matchBase,
                        walkSlots, walkState, info, tokens, blockTail);
   }
-  hipLaunchKernelGGL(k_block_bytes, dim3(nblocks), dim3(kAsmThreads), 0, s, blocks, maxChain, info, blockTail, ntok, blockBytes);
+  hipLaunchKernelGGL(k_block_bytes, dim3(nblocks), dim3(kAsmThreads), 0, s, blocks, maxChain, info, blockTail, ntok, blockBytes,
+                     status);
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, blockBytes, nblocks, offsets);
   if (nwalk)
     hipLaunchKernelGGL(k_write_seg, dim3(segGrid), dim3(64 * kSegWaves), 0, s, in, blocks, walkSegs, nwalk, walkState, info, tokens,

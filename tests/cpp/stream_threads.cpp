@@ -1,0 +1,137 @@
+// stream_threads.cpp -- the drop-in header (include/smallz4_amd.hpp) under load, for tests/test_stream.py.
+//
+//   stream_threads threads <level> <in1> <out1> [<in2> <out2> ...]
+//       one host thread per (in, out) pair, all calling smallz4::lz4 at the same time (the reference
+//       builds a fresh object per call, smallz4.h:56-64, so concurrent calls must not interfere)
+//   stream_threads big <level> <base> <reps> <out>
+//       one long stream through smallz4::lz4: <base> repeated <reps> times, repetition r with the
+//       8 bytes at offset (r * 7919) % size replaced by r (little endian); prints the library's
+//       device footprint (sz4_device_bytes of the pooled context) and the stream's length
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "smallz4_amd.hpp"
+
+namespace {
+
+std::vector<unsigned char> read_file(const char* path)
+{
+  std::vector<unsigned char> v;
+  FILE* f = fopen(path, "rb");
+  if (!f) {
+    perror(path);
+    exit(2);
+  }
+  unsigned char buf[1 << 16];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, f)) > 0) v.insert(v.end(), buf, buf + k);
+  fclose(f);
+  return v;
+}
+
+struct MemIn {
+  const std::vector<unsigned char>* data;
+  size_t at;
+};
+struct FileOut {
+  FILE* f;
+};
+
+size_t get_mem(void* data, size_t n, void* user)
+{
+  MemIn* m = static_cast<MemIn*>(user);
+  const size_t k = std::min(n, m->data->size() - m->at);
+  memcpy(data, m->data->data() + m->at, k);
+  m->at += k;
+  return k;
+}
+
+// both directions through one user pointer, as the reference's CLI does (smallz4.cpp:50-117)
+struct Job {
+  MemIn in;
+  FILE* out;
+};
+size_t get_job(void* data, size_t n, void* user) { return get_mem(data, n, &static_cast<Job*>(user)->in); }
+void send_job(const void* data, size_t n, void* user)
+{
+  if (n) fwrite(data, 1, n, static_cast<Job*>(user)->out);
+}
+
+// the long synthetic stream
+struct Big {
+  const std::vector<unsigned char>* base;
+  uint64_t reps, pos, total;
+  FILE* out;
+  uint64_t sent;
+};
+size_t get_big(void* data, size_t n, void* user)
+{
+  Big* b = static_cast<Big*>(user);
+  unsigned char* d = static_cast<unsigned char*>(data);
+  const uint64_t size = b->base->size();
+  size_t k = 0;
+  while (k < n && b->pos < b->total) {
+    const uint64_t r = b->pos / size, o = b->pos % size;
+    const uint64_t take = std::min<uint64_t>(n - k, size - o);
+    memcpy(d + k, b->base->data() + o, take);
+    // patch: the 8 bytes at (r * 7919) % size hold r
+    const uint64_t p = (r * 7919) % size;
+    for (uint64_t j = 0; j < 8; j++) {
+      const uint64_t q = p + j;
+      if (q >= o && q < o + take && q < size) d[k + (q - o)] = (unsigned char)(r >> (8 * j));
+    }
+    k += take;
+    b->pos += take;
+  }
+  return k;
+}
+void send_big(const void* data, size_t n, void* user)
+{
+  Big* b = static_cast<Big*>(user);
+  if (n) fwrite(data, 1, n, b->out);
+  b->sent += n;
+}
+
+}  // namespace
+
+int main(int argc, char** argv)
+{
+  if (argc < 3) return 2;
+  const int level = atoi(argv[2]);
+  const unsigned short chain = level >= 9 ? 65535 : (unsigned short)level;
+  if (std::string(argv[1]) == "threads") {
+    const int n = (argc - 3) / 2;
+    std::vector<std::vector<unsigned char>> inputs(n);
+    std::vector<Job> jobs(n);
+    for (int i = 0; i < n; i++) {
+      inputs[i] = read_file(argv[3 + 2 * i]);
+      jobs[i].in = MemIn{&inputs[i], 0};
+      jobs[i].out = fopen(argv[4 + 2 * i], "wb");
+    }
+    std::vector<std::thread> threads;
+    for (int i = 0; i < n; i++)
+      threads.emplace_back([&, i]() { smallz4::lz4(get_job, send_job, chain, false, &jobs[i]); });
+    for (auto& t : threads) t.join();
+    for (auto& j : jobs) fclose(j.out);
+    return 0;
+  }
+  if (std::string(argv[1]) == "big" && argc >= 6) {
+    std::vector<unsigned char> base = read_file(argv[3]);
+    Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, fopen(argv[5], "wb"), 0};
+    b.total = b.reps * base.size();
+    smallz4::lz4(get_big, send_big, chain, false, &b);
+    fclose(b.out);
+    // the footprint of the pooled context the call used (handed back to the pool, borrowed again)
+    sz4_ctx* c = NULL;
+    sz4_acquire(&c, getenv("SMALLZ4_AMD_DEVICE") ? atoi(getenv("SMALLZ4_AMD_DEVICE")) : 0);
+    printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu}\n", (unsigned long long)b.total,
+           (unsigned long long)b.sent, (unsigned long long)sz4_device_bytes(c));
+    sz4_release(c);
+    return 0;
+  }
+  return 2;
+}

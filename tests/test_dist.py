@@ -65,3 +65,32 @@ def test_shard_range_partitions():
             for (a, b), (c, d) in zip(ranges, ranges[1:]):
                 assert b == c and a <= b
                 assert a % 65536 == 0
+
+
+def test_bench_gpus2_dry_run_starts_two_ranks():
+    """`bench.py --gpus 2` outside torch.distributed starts two ranks itself (torch.distributed.run
+    child); in the HIP-free dry run each rank compresses its block range of ONE input (the oracle as
+    the block compressor) and the rank-ordered parts equal the single-process frame."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for workload, mb in (("enwik9", 0.3), ("zeros_urandom", 0.6)):
+        r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run",
+                            "--workload", workload, "--mb", str(mb)],
+                           capture_output=True, text=True, timeout=600, cwd=root)
+        assert r.returncode == 0, r.stderr[-2000:]
+        line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+        rec = json.loads(line)
+        assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["parts_equal_single"], rec
+        assert rec["input_bytes"] == 2 * int(mb * 1e6)
+
+
+def test_range_generators_are_slices_of_one_input():
+    from smallz4_amd import synth
+    a = synth.zeros_urandom_range(0, 1 << 20)
+    assert synth.zeros_urandom_range(123457, 777777) == a[123457:777777]
+    assert a[:131072] == bytes(131072) and a[131072:262144] != bytes(131072)
+    seg = synth.ENWIK9_SEGMENT
+    x = synth.enwik9_like_range(seg - 1000, seg + 1000)
+    assert x == synth.enwik9_like_range(seg - 1000, seg) + synth.enwik9_like_range(seg, seg + 1000)

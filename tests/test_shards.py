@@ -1,0 +1,81 @@
+"""The sharded configurations on one MI355X: BASELINE configs[3] (enwik9-shaped, 64 KiB blocks) and
+configs[4] (zeros/urandom, 256 KiB blocks) as the 8-GPU run splits them, one rank's slice at full
+size.  Blocks are independent, so a rank's part is bare blocks and the rank-ordered parts concatenate
+to the single-GPU frame.  Full-size slices are checked through size-independent properties (device
+round trip, the size-word walk) plus the oracle on a fixed sample of blocks.  Run with -m gpu."""
+import numpy as np
+import pytest
+
+from oracle import pyoracle
+from smallz4_amd import shard, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_roundtrip(compressor, part: bytes, data: bytes):
+    import torch
+    frame = shard.HEADER + part + shard.END_MARK
+    f = torch.frombuffer(bytearray(frame), dtype=torch.uint8).cuda()
+    want = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    out = torch.empty(len(data), dtype=torch.uint8, device="cuda")
+    n = compressor.unlz4_device(f.data_ptr(), len(frame), out.data_ptr(), len(data))
+    torch.cuda.synchronize()
+    return n == len(data) and bool(torch.equal(out, want))
+
+
+def _spans(part: bytes):
+    spans, pos = [], 0
+    while pos + 4 <= len(part):
+        word = int.from_bytes(part[pos:pos + 4], "little")
+        spans.append((pos, 4 + (word & 0x7FFFFFFF)))
+        pos += 4 + (word & 0x7FFFFFFF)
+    assert pos == len(part)
+    return spans
+
+
+def test_two_contexts_shards_concatenate_to_single_frame(compressor):
+    """Two ranks' work on one GPU: two contexts, one per shard of ONE input, header 'none'."""
+    import smallz4_amd
+    data = synth.enwik9_like_range(0, 9_000_000)
+    bs = 65536
+    other = smallz4_amd.Compressor(device=0)
+    parts = []
+    for r, comp in enumerate((compressor, other)):
+        lo, hi = shard.shard_range(len(data), bs, r, 2)
+        parts.append(shard.frame_part(comp.compress_blocks(data[lo:hi], bs, 65535, header="none"), r, 2))
+    assert b"".join(parts) == compressor.compress_blocks(data, bs, 65535)
+    other.close()
+
+
+@pytest.mark.parametrize("workload,world,bs", [("enwik9", 8, 65536), ("zeros_urandom", 8, 262144)])
+def test_rank0_slice_full_size(compressor, workload, world, bs):
+    """Rank 0's slice of the 8-GPU configuration at full size: 125 MB of configs[3], 1.25 GiB of
+    configs[4]."""
+    if workload == "enwik9":
+        total = 125_000_000 * world
+        lo, hi = shard.shard_range(total, bs, 0, world)
+        data = synth.enwik9_like_range(lo, hi, seed=9, workers=8)
+    else:
+        total = (10 << 30)
+        lo, hi = shard.shard_range(total, bs, 0, world)
+        data = synth.zeros_urandom_range(lo, hi, seed=10)
+    before = compressor.device_bytes()
+    part = compressor.compress_blocks(data, bs, 65535, header="none")
+    spans = _spans(part)
+    assert len(spans) == (len(data) + bs - 1) // bs
+    assert _device_roundtrip(compressor, part, data)
+    # the oracle on a fixed sample of blocks, the first and the last included (a zeros/urandom block
+    # costs the oracle ~13 s -- its chain walk is quadratic in a run -- so that sample is smaller)
+    k = 24 if workload == "enwik9" else 3
+    idx = sorted(set(list(range(0, len(spans), max(1, len(spans) // k))) + [len(spans) - 1]))
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        want = list(ex.map(lambda i: pyoracle.oz_block(data[i * bs:(i + 1) * bs], 65535), idx))
+    for i, w in zip(idx, want):
+        o, n = spans[i]
+        assert part[o:o + n] == w, i
+    # HBM footprint of the context for this slice (grow-only scratch)
+    footprint = compressor.device_bytes()
+    print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
+          f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
+    assert footprint < 120 * len(data) + (1 << 30)

@@ -1,0 +1,181 @@
+"""The bounded-memory stream paths (sz4_lz4_stream / sz4_lz4 compressing chunk by chunk, and
+sz4_unlz4_stream decoding chunk by chunk) against the reference's golden vectors and the oracle.
+A chunk boundary must not change a byte: the carried 64 KiB window, the lookback cut and the previous
+block's shortcut intervals (smallz4.h:614-643, 798-805) and dictionary mode's tables all cross it.
+Also: reentrancy of the drop-in header (threads), and a multi-GiB stream with a fixed device
+footprint.  Run with -m gpu on an MI355X."""
+import hashlib
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import inputs
+from oracle import pyoracle
+from smallz4_amd import synth
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+M = 4 << 20  # MaxBlockSize
+
+
+@pytest.fixture
+def chunked(compressor):
+    """The compressor with one 4 MiB block per chunk: every block boundary is a chunk boundary."""
+    compressor.set_stream_chunk(M)
+    yield compressor
+    compressor.set_stream_chunk(0)
+
+
+def test_golden_vectors_one_block_per_chunk(chunked, golden):
+    for case in golden:
+        data = inputs.make(case["input"])
+        dictionary = inputs.make(case["dict"]) if "dict" in case else b""
+        frame = chunked.lz4(data, case["level"], dictionary, bool(case["legacy"]))
+        assert inputs.sha(frame) == case["out_sha256"], (case["name"], case["level"], case["legacy"])
+
+
+def _long_run_across(seed):
+    # a zero run of 300 000 bytes across the first block boundary: the shortcut interval of block 0
+    # reaches its end, so block 1's window must leave those positions out (the ghost slot)
+    return synth.enwik8_like(M - 150000, seed=seed) + bytes(300000) + synth.enwik8_like(M + 70000, seed=seed + 1)
+
+
+@pytest.mark.parametrize("chain", [2, 5, 7, 65535])
+def test_chunk_boundaries_match_oracle(chunked, chain):
+    cases = [
+        synth.enwik8_like(9 << 20, seed=60),
+        _long_run_across(61),
+        synth.enwik8_like(M - 20, seed=63) + bytes(100) + synth.enwik8_like(M + 5, seed=64),
+        synth.zeros_urandom(2 * M + 12345, run=131072, seed=65),
+    ]
+    for data in cases:
+        assert chunked.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+@pytest.mark.parametrize("chain", [3, 65535])
+def test_chunked_dictionary_and_legacy(chunked, chain, legacy):
+    """Dictionary mode carries the reference's hash table and both chains across chunks (their slots
+    are absolute positions mod 65536: chunks move by multiples of 65536)."""
+    data = synth.enwik8_like(2 * M + 300000, seed=66)
+    dictionary = synth.enwik8_like(50000, seed=67)
+    assert chunked.lz4(data, chain, dictionary, legacy) == pyoracle.oz_lz4(data, chain, dictionary, legacy)
+    assert chunked.lz4(data, chain, b"", legacy) == pyoracle.oz_lz4(data, chain, b"", legacy)
+
+
+def test_stream_callbacks_ragged_reads(chunked):
+    """getBytes may return fewer bytes than asked; the output and the call pattern stay the reference's."""
+    data = synth.enwik8_like(2 * M + 777, seed=68)
+    rng = np.random.default_rng(69)
+    pos = [0]
+
+    def read(n):
+        k = int(min(n, rng.integers(1, 70000), len(data) - pos[0]))
+        b = data[pos[0]:pos[0] + k]
+        pos[0] += k
+        return b
+
+    calls = []
+    chunked.lz4_stream(read, calls.append, 65535)
+    want = pyoracle.oz_lz4(data, 65535)
+    assert b"".join(calls) == want
+    # header, then per block 4 one-byte calls and the payload, then the end mark (smallz4.h:478-812)
+    nblocks = (len(data) + M - 1) // M
+    assert len(calls) == 1 + 5 * nblocks + 1
+    assert calls[0] == want[:7] and all(len(c) == 1 for c in calls[1:5]) and calls[-1] == b"\0\0\0\0"
+
+
+def test_stream_empty_and_tiny(compressor):
+    for data in (b"", b"a", b"abcdefghijkl"):
+        for legacy in (False, True):
+            out = []
+            compressor.lz4_stream(lambda n, d=[data]: d.pop() if d else b"", out.append, 65535, b"", legacy)
+            assert b"".join(out) == pyoracle.oz_lz4(data, 65535, b"", legacy)
+
+
+def _decode_stream(compressor, frame, dictionary=b""):
+    it = iter(frame)
+    pieces = []
+    compressor.unlz4_stream(lambda: next(it), pieces.append, dictionary)
+    return pieces
+
+
+@pytest.mark.parametrize("legacy", [False, True])
+def test_decoder_stream_chunks_and_flush_points(compressor, legacy):
+    compressor.set_stream_chunk(2 << 20)  # 1 MiB of frame per decode chunk
+    try:
+        data = synth.enwik8_like(3 * M + 1000, seed=70)
+        frame = pyoracle.oz_lz4(data, 65535, b"", legacy)
+        pieces = _decode_stream(compressor, frame)
+        assert b"".join(pieces) == data
+        # the reference flushes its 64 KiB history whenever it fills, and the remainder at the end
+        assert all(len(p) == 65536 for p in pieces[:-1]) and len(pieces[-1]) == len(data) % 65536
+        dictionary = synth.enwik8_like(90000, seed=71)
+        frame = pyoracle.oz_lz4(data[:300000], 6, dictionary, legacy)
+        assert b"".join(_decode_stream(compressor, frame, dictionary)) == pyoracle.oz_unlz4(frame, dictionary)
+    finally:
+        compressor.set_stream_chunk(0)
+
+
+def test_decoder_stream_rejects_like_the_reference(compressor):
+    from smallz4_amd._native import NativeError
+    with pytest.raises(NativeError, match="invalid signature"):
+        _decode_stream(compressor, b"\x00\x01\x02\x03" + bytes(20))
+    with pytest.raises(NativeError, match="version 1"):
+        _decode_stream(compressor, bytes([0x04, 0x22, 0x4D, 0x18, 0x80, 0x70, 0xDF]) + bytes(8))
+
+
+def _build_tool(tmp_path):
+    exe = tmp_path / "stream_threads"
+    subprocess.run(["hipcc", "-std=c++17", "-O2", "-pthread", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "stream_threads.cpp"), "-L", os.path.join(ROOT, "smallz4_amd", "lib"),
+                    "-lsmallz4_amd", "-Wl,-rpath," + os.path.join(ROOT, "smallz4_amd", "lib"), "-o", str(exe)], check=True)
+    return str(exe)
+
+
+def test_dropin_concurrent_threads(tmp_path):
+    """Four host threads call smallz4::lz4 at once (include/smallz4_amd.hpp): each gets a context of
+    its own from the library's pool, and each output equals the oracle's."""
+    exe = _build_tool(tmp_path)
+    datas = [synth.enwik8_like((1 << 20) * (k + 1) + 333 * k, seed=80 + k) for k in range(4)]
+    args = [exe, "threads", "9"]
+    for k, d in enumerate(datas):
+        (tmp_path / f"in{k}").write_bytes(d)
+        args += [str(tmp_path / f"in{k}"), str(tmp_path / f"out{k}")]
+    subprocess.run(args, check=True, timeout=300)
+    for k, d in enumerate(datas):
+        assert (tmp_path / f"out{k}").read_bytes() == pyoracle.oz_lz4(d, 65535), k
+
+
+def _big_input(base: bytes, reps: int) -> bytes:
+    buf = bytearray(base * reps)
+    size = len(base)
+    for r in range(reps):
+        p = (r * 7919) % size
+        for j in range(8):
+            if p + j < size:
+                buf[r * size + p + j] = (r >> (8 * j)) & 0xFF
+    return bytes(buf)
+
+
+def test_dropin_multi_gib_stream_fixed_footprint(tmp_path):
+    """2 GiB through smallz4::lz4 in 64 MiB chunks: the device footprint is that of one chunk, the
+    frame decodes to the input (oracle decoder), and its first blocks equal the oracle's stream."""
+    exe = _build_tool(tmp_path)
+    base = synth.enwik8_like(16 << 20, seed=90)
+    (tmp_path / "base").write_bytes(base)
+    reps = 128
+    r = subprocess.run([exe, "big", "9", str(tmp_path / "base"), str(reps), str(tmp_path / "big.lz4")],
+                       check=True, capture_output=True, text=True, timeout=600)
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["input_bytes"] == reps * len(base)
+    assert info["device_bytes"] < 8 << 30, info  # one 64 MiB chunk's scratch, not 2 GiB worth
+    frame = (tmp_path / "big.lz4").read_bytes()
+    assert len(frame) == info["output_bytes"]
+    data = _big_input(base, reps)
+    assert hashlib.sha256(pyoracle.oz_unlz4(frame, cap=len(data) + 16)).digest() == hashlib.sha256(data).digest()
+    head = pyoracle.oz_lz4(data[:3 * M], 65535)
+    assert frame[:len(head) - 4] == head[:-4]
