@@ -334,9 +334,9 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   // another sort/find/prep round (each round checks a longer prefix of it)
   for (uint32_t round = 0; c->dictBack < 0; round++) {
     if (maxChain > 0) {
-      // every target starts "unresolved" (pass 2 picks up what pass 1 does not write: shortcut intervals)
-      if ((e = hipMemsetAsync(c->mlen.p, 0xFF, c->hBlocks.back().end * 4, s)) ||
-          (e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
+      // k_find_sorted writes every target (shortcut-interval targets "unresolved", for pass 2); its
+      // marker bits are OR-ed in
+      if ((e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
         return c->fail(SZ4_E_DEVICE, "clear matches", e);
       // k_find_sorted sorts its own segment first unless SZ4_SEPARATE_SORT=1
       if (c->separateSort)

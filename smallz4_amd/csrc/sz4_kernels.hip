@@ -328,19 +328,25 @@ __global__ __launch_bounds__(256) void k_runs(const uint8_t* __restrict__ in, co
 
 // ================================================================================================
 // k_sort: one 1024-thread workgroup per segment.  Groups the inserted positions of the window
-// [w0, s1) by their four key bytes, positions ascending inside a group: one stable LSD counting
-// sort over a 16-bit hash of the key (two 8-bit passes) on packed 32-bit elements
+// [w0, s1) by their four key bytes, positions ascending inside a group: one stable LSD radix sort
+// over a 16-bit hash of the key (two 8-bit passes) on packed 32-bit elements
 // (hash << posBits | position - w0).  Different keys that share a hash land in the same group;
 // the searches compare the four key bytes themselves, so the candidate sets stay exact.  After
 // the sort, the candidates of target p are the same-key entries just below p's slot -- the
 // reference's previousExact chain of p, nearest first.
+// Every pass goes through LDS a tile of kSortTile elements at a time: the tile is ranked (stable:
+// waves take consecutive sub-ranges, lanes rank by ballot), reordered by digit in LDS, and written
+// out as one contiguous run per digit -- whole cache lines instead of one scattered dword per
+// element.  The digit totals of both passes come from one histogram pass over the text, and pass 0
+// reads its keys straight from the text (no element array is written before it).
 // Outputs (in bufB, which the sort no longer needs): per slot the window position and the slot
-// where its hash group starts (u16 each when the window fits 16 bits, u32 otherwise); per target
-// its slot.
+// where its hash group starts (u16 each when the window fits 16 bits, u32 otherwise).  The slot of a
+// target is written by k_find_sorted for the targets it hands to pass 2 only.
 // ================================================================================================
 constexpr int kSortThreads = 1024;
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr uint32_t kSortBatch = 8;  // loads in flight per lane in the latency-bound loops
+constexpr uint32_t kSortBatch = 8;                          // elements per lane per tile
+constexpr uint32_t kSortTile = kSortThreads * kSortBatch;   // 8192 elements staged per tile
 
 __device__ __forceinline__ uint32_t pos_bits(uint32_t W) { return W <= 65536u ? 16u : 17u; }
 __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
@@ -348,27 +354,42 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
   return (key * 2654435761u) >> posBits;  // top (32 - posBits) bits of a multiplicative hash
 }
 
-// k_sort's shared memory.  When k_find_sorted sorts its own segment it lives in the window buffer,
-// which is loaded only after the sort.
+// k_sort's shared memory (57 KB).  When k_find_sorted sorts its own segment it lives in the window
+// buffer, which is loaded only after the sort.
 struct SortLds {
-  uint32_t hist[kSortWaves][256];
+  uint32_t tile[kSortTile];        // a tile in digit order; the histogram pass's second table; the scan
+  uint32_t cnt[kSortWaves][256];   // per wave and digit: count, then offset inside the tile
+  uint32_t gOff[2][256];           // per pass and digit: next output slot
+  uint32_t tileStart[256], tileCnt[256];
   uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
-  uint32_t scan[kSortThreads];
-  uint32_t wsum[4];
+  uint32_t wsum[kSortWaves];
   uint32_t nEx;
 };
 
+// exclusive prefix sum over the 256 digits of v (threads 0..255 hold one digit each), result in out
+__device__ __forceinline__ void digit_scan(uint32_t v, uint32_t* out, uint32_t* wsum)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t incl = 0;
+  if (tid < 256) {
+    incl = wave_incl_scan_add(v);
+    if (lane == 63) wsum[wave] = incl;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; w++) base += wsum[w];
+    out[tid] = base + incl - v;
+  }
+  __syncthreads();
+}
+
 __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, const Segment& S, const Block& B,
                                              const Interval* __restrict__ ivAll, const uint32_t* __restrict__ ivCount,
-                                             uint2* bufA, uint2* bufB, uint32_t* rank, SortLds& L)
+                                             uint2* bufA, uint2* bufB, SortLds& L)
 {
-  auto& hist = L.hist;
-  auto& wsum = L.wsum;
-  auto& exLo = L.exLo;
-  auto& exHi = L.exHi;
-  auto& nEx = L.nEx;
-  auto& s_scan = L.scan;
-  const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
 
   // positions excluded from insertion: shortcut intervals of this block and of the previous one
   if (tid == 0) {
@@ -380,119 +401,133 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
       for (uint32_t j = 0; j < ivCount[blkIds[t]]; j++) {
         uint64_t lo = iv[j].lo > S.w0 ? iv[j].lo : S.w0;
         uint64_t hi = iv[j].hi < S.s1 ? iv[j].hi : S.s1;
-        if (lo < hi) { exLo[k] = lo; exHi[k] = hi; k++; }
+        if (lo < hi) { L.exLo[k] = lo; L.exHi[k] = hi; k++; }
       }
     }
-    nEx = k;
+    L.nEx = k;
   }
   __syncthreads();
-  const uint32_t ne = nEx;
+  const uint32_t ne = L.nEx;
   uint64_t excluded = 0;
-  for (uint32_t j = 0; j < ne; j++) excluded += exHi[j] - exLo[j];
+  for (uint32_t j = 0; j < ne; j++) excluded += L.exHi[j] - L.exLo[j];
 
-  uint32_t* src = reinterpret_cast<uint32_t*>(bufA + S.elemOff);
-  uint32_t* dst = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   const uint32_t W = (uint32_t)(S.s1 - S.w0);
   const uint32_t E = W - (uint32_t)excluded;
   const uint32_t pb = pos_bits(W);
   const uint32_t posMask = (1u << pb) - 1u;
+  // element i of the compacted window: its position (intervals skipped; they are ordered and disjoint)
+  auto elem_at = [&](uint32_t i) -> uint32_t {
+    uint64_t q = S.w0 + i;
+    for (uint32_t j = 0; j < ne; j++)
+      if (q >= L.exLo[j]) q += L.exHi[j] - L.exLo[j];
+    const uint32_t r = (uint32_t)(q - S.w0);
+    return (key_hash(gload4(in, q), pb) << pb) | r;
+  };
 
-  // 1. packed elements in position order (intervals compacted out); loads issued kSortBatch at a time
-  for (uint32_t r0 = tid; r0 < W; r0 += kSortThreads * kSortBatch) {
-    uint32_t key[kSortBatch];
-#pragma unroll
-    for (uint32_t u = 0; u < kSortBatch; u++) {
-      const uint32_t r = r0 + u * kSortThreads;
-      key[u] = r < W ? gload4(in, S.w0 + r) : 0u;
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kSortBatch; u++) {
-      const uint32_t r = r0 + u * kSortThreads;
-      if (r >= W) break;
-      const uint64_t q = S.w0 + r;
-      uint32_t idx = r;
-      bool skip = false;
-      for (uint32_t j = 0; j < ne; j++) {
-        if (q >= exHi[j]) idx -= (uint32_t)(exHi[j] - exLo[j]);
-        else if (q >= exLo[j]) skip = true;
-      }
-      if (!skip) src[idx] = (key_hash(key[u], pb) << pb) | r;
-    }
+  // 1. digit totals of both passes: per-wave histograms (cnt: pass 0, tile: pass 1), then offsets
+  for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) {
+    (&L.cnt[0][0])[i] = 0;
+    L.tile[i] = 0;
   }
   __syncthreads();
+  for (uint32_t i0 = tid; i0 < E; i0 += kSortThreads * kSortBatch) {
+    uint32_t e[kSortBatch];
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++) e[u] = i0 + u * kSortThreads < E ? elem_at(i0 + u * kSortThreads) : 0u;
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++)
+      if (i0 + u * kSortThreads < E) {
+        atomicAdd(&L.cnt[wave][(e[u] >> pb) & 255u], 1u);
+        atomicAdd(&L.tile[wave * 256 + ((e[u] >> (pb + 8)) & 255u)], 1u);
+      }
+  }
+  __syncthreads();
+  {
+    uint32_t h0 = 0, h1 = 0;
+    if (tid < 256)
+      for (uint32_t w = 0; w < kSortWaves; w++) {
+        h0 += L.cnt[w][tid];
+        h1 += L.tile[w * 256 + tid];
+      }
+    digit_scan(h0, L.gOff[0], L.wsum);
+    digit_scan(h1, L.gOff[1], L.wsum);
+  }
 
-  // 2. two stable counting passes over the hash bits (low byte first)
-  const uint32_t chunk = (((E + kSortWaves - 1) / kSortWaves) + 63) & ~63u;
-  const uint32_t b0 = wave * chunk < E ? wave * chunk : E;
-  const uint32_t b1 = b0 + chunk < E ? b0 + chunk : E;
-  for (int pass = 0; pass < 2; pass++) {
+  // 2. two stable passes (low digit first), each tile ranked and reordered in LDS
+  uint32_t* src = reinterpret_cast<uint32_t*>(bufB + S.elemOff);  // pass 1 reads what pass 0 wrote
+  for (uint32_t pass = 0; pass < 2; pass++) {
+    uint32_t* dst = reinterpret_cast<uint32_t*>((pass == 0 ? bufB : bufA) + S.elemOff);
     const uint32_t sh = pb + 8u * pass;
-    for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) (&hist[0][0])[i] = 0;
-    __syncthreads();
-    for (uint32_t i0 = b0 + lane; i0 < b1; i0 += 64 * kSortBatch) {
-      uint32_t v[kSortBatch];
-#pragma unroll
-      for (uint32_t u = 0; u < kSortBatch; u++) v[u] = i0 + 64 * u < b1 ? src[i0 + 64 * u] : 0u;
-#pragma unroll
-      for (uint32_t u = 0; u < kSortBatch; u++)
-        if (i0 + 64 * u < b1) atomicAdd(&hist[wave][(v[u] >> sh) & 255u], 1u);
-    }
-    __syncthreads();
-    uint32_t total = 0;
-    if (tid < 256) {
-      for (int w = 0; w < kSortWaves; w++) {
-        const uint32_t c = hist[w][tid];
-        hist[w][tid] = total;
-        total += c;
-      }
-      const uint32_t incl = wave_incl_scan_add(total);
-      if (lane == 63) wsum[wave] = incl;
-      total = incl - total;  // exclusive within this wave
-    }
-    __syncthreads();
-    if (tid < 256) {
-      uint32_t base = total;
-      for (uint32_t w = 0; w < wave; w++) base += wsum[w];
-      for (int w = 0; w < kSortWaves; w++) hist[w][tid] += base;
-    }
-    __syncthreads();
-    for (uint32_t base0 = b0; base0 < b1; base0 += 64 * kSortBatch) {
-      uint32_t v[kSortBatch];
+    for (uint32_t t0 = 0; t0 < E; t0 += kSortTile) {
+      const uint32_t tn = E - t0 < kSortTile ? E - t0 : kSortTile;
+      for (uint32_t d = tid; d < kSortWaves * 256; d += kSortThreads) (&L.cnt[0][0])[d] = 0;
+      __syncthreads();
+      // wave w ranks elements [t0 + w * 512, +512), 64 per batch; (element, digit, rank in the wave)
+      uint32_t e[kSortBatch], rk[kSortBatch];
+      const uint32_t wb = t0 + wave * (64 * kSortBatch);
 #pragma unroll
       for (uint32_t u = 0; u < kSortBatch; u++) {
-        const uint32_t i = base0 + 64 * u + lane;
-        v[u] = i < b1 ? src[i] : 0u;
+        const uint32_t i = wb + 64 * u + lane;
+        e[u] = i < t0 + tn ? (pass == 0 ? elem_at(i) : src[i]) : 0u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kSortBatch; u++) {
-        const uint32_t base = base0 + 64 * u;
-        if (base >= b1) break;
-        const uint32_t i = base + lane;
-        const bool valid = i < b1;
-        const uint32_t e = v[u];
-        const uint32_t d = (e >> sh) & 255u;
+        const uint32_t i = wb + 64 * u + lane;
+        const bool valid = i < t0 + tn;
+        const uint32_t d = (e[u] >> sh) & 255u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; b++) {
           const uint64_t m = __ballot((d >> b) & 1);
           peers &= ((d >> b) & 1) ? m : ~m;
         }
+        rk[u] = 0;
         if (valid) {
-          const uint32_t rk = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-          const uint32_t off = hist[wave][d];
-          dst[off + rk] = e;
-          if (rk == 0) hist[wave][d] = off + (uint32_t)__popcll(peers);
+          const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+          rk[u] = L.cnt[wave][d] + below;
         }
+        // the lowest lane of each digit advances the wave's count (after every lane has read it)
+        const bool leader = valid && (peers & ((1ull << lane) - 1ull)) == 0;
+        if (leader) L.cnt[wave][d] += (uint32_t)__popcll(peers);
       }
+      __syncthreads();
+      // tile layout: digit-major, waves in order inside a digit
+      uint32_t tc = 0;
+      if (tid < 256)
+        for (uint32_t w = 0; w < kSortWaves; w++) {
+          const uint32_t c = L.cnt[w][tid];
+          L.cnt[w][tid] = tc;
+          tc += c;
+        }
+      digit_scan(tc, L.tileStart, L.wsum);
+      if (tid < 256) {
+        L.tileCnt[tid] = tc;
+        const uint32_t st = L.tileStart[tid];
+        for (uint32_t w = 0; w < kSortWaves; w++) L.cnt[w][tid] += st;
+      }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t u = 0; u < kSortBatch; u++) {
+        const uint32_t i = wb + 64 * u + lane;
+        if (i < t0 + tn) L.tile[L.cnt[wave][(e[u] >> sh) & 255u] + rk[u]] = e[u];
+      }
+      __syncthreads();
+      // one contiguous run per digit
+      for (uint32_t i = tid; i < tn; i += kSortThreads) {
+        const uint32_t v = L.tile[i];
+        const uint32_t d = (v >> sh) & 255u;
+        dst[L.gOff[pass][d] + (i - L.tileStart[d])] = v;
+      }
+      __syncthreads();
+      if (tid < 256) L.gOff[pass][tid] += L.tileCnt[tid];
+      __syncthreads();
     }
-    __syncthreads();
-    uint32_t* t = src;
     src = dst;
-    dst = t;
   }
-  // two passes: sorted elements are back in bufA; bufB receives the per-slot arrays
+  // the sorted elements are in bufA; bufB receives the per-slot arrays
   // 3. hash-group starts: tiles of 1024 consecutive slots, inclusive max-scan of (start slot + 1)
-  //    carried across tiles; every access coalesced; slot of every target
+  //    carried across tiles; every access coalesced
+  uint32_t* s_scan = L.tile;
   const bool small = W <= 65536u;  // == compact_small(S)
   uint16_t* pos16 = reinterpret_cast<uint16_t*>(bufB + S.elemOff);
   uint16_t* gs16 = pos16 + E;
@@ -525,8 +560,6 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
         pos32[s] = rel;
         gs32[s] = g;
       }
-      const uint64_t q = S.w0 + rel;
-      if (q >= S.s0) rank[S.rankOff + (q - S.s0)] = s;
     }
     for (uint32_t w = wave; w < kSortWaves; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
     carry = pre;
@@ -537,12 +570,12 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
 __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                        const uint32_t* __restrict__ ivCount, uint2* __restrict__ bufA,
-                                                       uint2* __restrict__ bufB, uint32_t* __restrict__ rank)
+                                                       uint2* __restrict__ bufB)
 {
   __shared__ SortLds lds;
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
-  sort_segment(in, S, B, ivAll, ivCount, bufA, bufB, rank, lds);
+  sort_segment(in, S, B, ivAll, ivCount, bufA, bufB, lds);
 }
 
 // ================================================================================================
@@ -634,6 +667,12 @@ constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_long9
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
+// k_find_sorted's results leave in text order, tiles of kOutTile positions staged in LDS
+constexpr uint32_t kOutTileBits = 14;
+constexpr uint32_t kOutTile = 1u << kOutTileBits;    // 64 KiB of LDS as u32
+constexpr uint32_t kOutTiles = 65536u / kOutTile;    // a segment has at most 65536 targets
+constexpr uint32_t kOutLong = 0xFFFFu;               // packed length: long, finished by pass 2
+constexpr uint32_t kOutUnsearched = 0xFFFEu;         // not a sorted target (shortcut interval)
 
 // per-slot arrays written by k_sort: u16 when the segment's window fits 16 bits (same predicate there)
 __device__ __forceinline__ bool compact_small(const Segment& S) { return S.s1 - S.w0 <= 65536u; }
@@ -658,6 +697,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
   __shared__ uint32_t s_long;
+  __shared__ uint32_t s_tileCnt[kOutTiles];
   // -9: per wavefront, candidates whose first 12 bytes match (lane << 17 | slot) and the best
   // exact key of each lane among them
   __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
@@ -689,9 +729,15 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
     // k_sort's work for this segment first, its shared memory in the (not yet loaded) window
     // buffer: the latency-bound sort of one workgroup overlaps the issue-bound search of the other
     // workgroup on the CU, and the sorted slots it writes are read back while L2-warm
-    sort_segment(in, S, B, ivAll, ivCount, sortA, compactAll, rankOut, *reinterpret_cast<SortLds*>(win));
+    sort_segment(in, S, B, ivAll, ivCount, sortA, compactAll, *reinterpret_cast<SortLds*>(win));
     __syncthreads();
   }
+  // results go out in text order through LDS (section at the end): during the search every target's
+  // (position, result) is appended to the bucket of its 16 Ki-position tile, in the sort's scratch
+  // (free now); s_tileCnt counts the entries per tile
+  uint2* bucket = sortA + S.elemOff;
+  const uint32_t nTargets = (uint32_t)(S.s1 - S.s0);
+  if (tid < kOutTiles) s_tileCnt[tid] = 0;
 
 #if SZ4_DIAG == 3
   const uint64_t t0 = __builtin_readcyclecounter();
@@ -1000,16 +1046,71 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         }
       }
     }
-    if (active) {
-      const uint64_t idx = p - matchBase;
-      mlen[idx] = isLong ? kLongMatch : (bestDist ? bestLen : 0u);
-      mdist[idx] = (uint16_t)(big ? 0u : bestDist);  // pass 2's seed: the nearest candidate at the cap
-      if (isLong && unlimited) atomicOr(&longBits[idx >> 5], 1u << (idx & 31));
+    // the result, packed: length (or kOutLong: pass 2 finishes it) << 16 | distance (for a long
+    // target pass 2's seed: the nearest candidate at the cap), appended to its tile's bucket
+    {
+      const uint32_t rel = active ? (uint32_t)(p - S.s0) : 0u;
+      const uint32_t packed = ((isLong ? kOutLong : (bestDist ? bestLen : 0u)) << 16) | (big ? 0u : (bestDist & 0xFFFFu));
+#pragma unroll
+      for (uint32_t k = 0; k < kOutTiles; k++) {
+        const uint64_t m = __ballot(active && (rel >> kOutTileBits) == k);
+        if (m) {
+          uint32_t at = 0;
+          if (lane == (uint32_t)__builtin_ctzll(m)) at = atomicAdd(&s_tileCnt[k], (uint32_t)__popcll(m));
+          at = (uint32_t)__builtin_amdgcn_readlane((int)at, (int)__builtin_ctzll(m));
+          if ((m >> lane) & 1ull) {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            bucket[(k << kOutTileBits) + at + below] = make_uint2(rel, packed);
+          }
+        }
+      }
+      // pass 2 finds a long target's candidates from its slot
+      if (active && isLong) rankOut[S.rankOff + rel] = slot;
     }
     if (unlimited && __ballot(active && isLong) && lane == 0) s_long = 1;
   }
   __syncthreads();
   if (tid == 0) segLong[blockIdx.x] = s_long;
+
+  // results in text order: tile by tile, the bucket is scattered into LDS (the window is free now)
+  // and written out coalesced -- mlen u32, mdist u16 and pass 2's marker bits.  Targets no bucket
+  // holds (shortcut intervals, never sorted) stay unresolved for pass 2.
+  uint32_t* otile = win;
+  for (uint32_t k = 0; k * kOutTile < nTargets; k++) {
+    const uint32_t t0 = k * kOutTile, tn = nTargets - t0 < kOutTile ? nTargets - t0 : kOutTile;
+    for (uint32_t i = tid; i < tn; i += kFindThreads) otile[i] = kOutUnsearched << 16;
+    __syncthreads();
+    const uint32_t cnt = s_tileCnt[k];
+    const uint2* bk = bucket + t0;
+    for (uint32_t i = tid; i < cnt; i += kFindThreads) {
+      const uint2 v = bk[i];
+      otile[v.x - t0] = v.y;
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < tn; i0 += kFindThreads) {
+      const uint32_t i = i0 + tid;
+      const bool in = i < tn;
+      const uint32_t v = in ? otile[i] : 0u;
+      const uint32_t len = v >> 16;
+      const uint64_t idx = S.s0 + t0 + i - matchBase;
+      if (in) {
+        mlen[idx] = len >= kOutUnsearched ? kLongMatch : len;
+        mdist[idx] = (uint16_t)(v & 0xFFFFu);
+      }
+      // marker bits of long pass-1 targets (-9): 64 consecutive positions per wave
+      const uint64_t m = __ballot(in && unlimited && len == kOutLong);
+      if (m && lane == 0) {
+        const uint64_t b0 = S.s0 + t0 + (i0 + (tid & ~63u)) - matchBase;
+        const uint32_t sh = (uint32_t)(b0 & 31);
+        uint32_t* w = longBits + (b0 >> 5);
+        const uint64_t lo = m << sh;  // bits b0 .. b0 + 63 over words w[0..2]
+        if ((uint32_t)lo) atomicOr(&w[0], (uint32_t)lo);
+        if ((uint32_t)(lo >> 32)) atomicOr(&w[1], (uint32_t)(lo >> 32));
+        if (sh && (uint32_t)(m >> (64 - sh))) atomicOr(&w[2], (uint32_t)(m >> (64 - sh)));
+      }
+    }
+    __syncthreads();
+  }
 #if SZ4_DIAG == 3
   const uint64_t t2 = __builtin_readcyclecounter();
   const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
@@ -3343,8 +3444,8 @@ void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Inter
 void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
                  const uint32_t* ivCount, uint2* elemA, uint2* elemB, uint32_t* rank, hipStream_t s)
 {
-  if (nsegs)
-    hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB, rank);
+  (void)rank;  // written by k_find_sorted for the targets pass 2 takes
+  if (nsegs) hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB);
 }
 
 uint32_t find_lds_bytes() { return 65536 + 16; }
@@ -3357,6 +3458,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                  bool fuseSort, hipStream_t s)
 {
   static_assert(sizeof(SortLds) <= 65536, "the fused sort's shared memory must fit the window buffer");
+  static_assert(kOutTile * 4u <= 65536u + 16u, "a result tile must fit the window buffer");
   if (!nsegs) return;
   const bool unlimited = maxChain >= 65535u;
   if (ldsWindow) {
@@ -3379,8 +3481,10 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                          compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
   } else {
     if (pass == 1) {
-      hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
-      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+      // the sort and the text-order result tiles use the same buffer: at least 64 KiB
+      const uint32_t lds = hybridLds > kOutTile * 4u ? hybridLds : kOutTile * 4u;
+      hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), lds, s, in, segs, blocks, iv, ivCount,
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {

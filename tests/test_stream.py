@@ -37,22 +37,20 @@ def test_golden_vectors_one_block_per_chunk(chunked, golden):
         assert inputs.sha(frame) == case["out_sha256"], (case["name"], case["level"], case["legacy"])
 
 
-def _long_run_across(seed):
-    # a zero run of 300 000 bytes across the first block boundary: the shortcut interval of block 0
-    # reaches its end, so block 1's window must leave those positions out (the ghost slot)
-    return synth.enwik8_like(M - 150000, seed=seed) + bytes(300000) + synth.enwik8_like(M + 70000, seed=seed + 1)
+CASES = {
+    "text9m": lambda: synth.enwik8_like(9 << 20, seed=60),
+    # a zero run of 110 000 bytes across the first block boundary: the same-letter shortcut interval
+    # of block 0 reaches its end, so block 1's window must leave those positions out (the ghost slot)
+    "run_across": lambda: synth.enwik8_like(M - 40000, seed=61) + bytes(110000) + synth.enwik8_like(M + 70000, seed=62),
+    "edge": lambda: synth.enwik8_like(M - 20, seed=63) + bytes(100) + synth.enwik8_like(M + 5, seed=64),
+}
 
 
+@pytest.mark.parametrize("case", sorted(CASES))
 @pytest.mark.parametrize("chain", [2, 5, 7, 65535])
-def test_chunk_boundaries_match_oracle(chunked, chain):
-    cases = [
-        synth.enwik8_like(9 << 20, seed=60),
-        _long_run_across(61),
-        synth.enwik8_like(M - 20, seed=63) + bytes(100) + synth.enwik8_like(M + 5, seed=64),
-        synth.zeros_urandom(2 * M + 12345, run=131072, seed=65),
-    ]
-    for data in cases:
-        assert chunked.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
+def test_chunk_boundaries_match_oracle(chunked, chain, case):
+    data = CASES[case]()
+    assert chunked.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
 
 
 @pytest.mark.parametrize("legacy", [False, True])
