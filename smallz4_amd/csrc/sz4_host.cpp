@@ -131,6 +131,7 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf chunkOut;             // stream path: one chunk's blocks
+  DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
   // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
@@ -164,7 +165,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &dictLast, &dictPrevH, &dictPrevX, &chunkOut,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
             &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut};
   }
 
@@ -356,7 +357,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel.as<uint32_t>(),
-                c->status.as<int>(), s);
+                c->longFlag.as<uint32_t>(), c->status.as<int>(), s);
     if (maxChain == 0 || maxChain > (uint32_t)kLazyMax) break;
     int st = 0;
     if ((e = hipMemcpyAsync(&st, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
@@ -365,6 +366,14 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
     if (round > 2 * kMaxIv + 2) return c->fail(SZ4_E_DEVICE, "shortcut intervals did not settle");
     if ((e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
       return c->fail(SZ4_E_DEVICE, "prep", e);
+  }
+  if (maxChain > 0 && maxChain <= (uint32_t)kLazyMax && c->dictBack < 0) {
+    // greedy/lazy: the reference's skip bookkeeping, in parallel for blocks without shortcut intervals
+    // (the others were replayed by k_prep); the token walk's state array is free until k_walk
+    if ((e = c->lazySlots.reserve(c->hWalk.size() * lazy_slots_per_walk() * 4ull + 64)))
+      return c->fail(SZ4_E_NOMEM, "lazy replay slots", e);
+    launch_lazy(dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), dIvN, c->longFlag.as<uint32_t>(),
+                c->mlen.as<uint32_t>(), 0, c->lazySlots.as<uint32_t>(), c->walkState.as<uint4>(), c->status.as<int>(), s);
   }
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),

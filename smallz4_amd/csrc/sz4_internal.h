@@ -115,7 +115,15 @@ void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint3
 // k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
 // corrected, run sort/find/prep again
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
-                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, int* status, hipStream_t s);
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, const uint32_t* longFlag, int* status,
+                 hipStream_t s);
+// greedy/lazy levels: the parallel replay of the reference's skip bookkeeping for blocks without
+// shortcut intervals (k_lazy_walk / k_lazy_fix / k_lazy_clear); slots: lazy_slots_per_walk() u32 per
+// walk sub-segment, state: one uint4 per walk sub-segment
+void launch_lazy(const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk, const uint32_t* ivCount,
+                 const uint32_t* longFlag, uint32_t* mlen, uint64_t matchBase, uint32_t* slots, uint4* state, int* status,
+                 hipStream_t s);
+uint32_t lazy_slots_per_walk();
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,

@@ -667,6 +667,8 @@ constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_long9
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
+constexpr uint32_t kFlagRmq = 1;   // longFlag: the block has matches of kRmqLen+ (other than same-letter runs)
+constexpr uint32_t kFlagRun = 2;   // longFlag: a distance-1 match longer than MaxSameLetter (bounded chains)
 // k_find_sorted's results leave in text order, tiles of kOutTile positions staged in LDS
 constexpr uint32_t kOutTileBits = 14;
 constexpr uint32_t kOutTile = 1u << kOutTileBits;    // 64 KiB of LDS as u32
@@ -1370,7 +1372,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     }
     // the parse keeps range minima for blocks with matches of kRmqLen+ (other than same-letter runs)
     const bool rmqLen = lane < cnt && pass1Len == kLongMatch && resLen >= kRmqLen && !(resDist == 1u && resLen >= kSameLetter);
-    if (__ballot(rmqLen) && lane == 0) atomicOr(&longFlag[S.block], 1u);
+    if (__ballot(rmqLen) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
+    // a distance-1 match beyond MaxSameLetter: the next position may take the same-letter shortcut
+    // (smallz4.h:631-643), so the greedy/lazy replay of this block stays in k_prep
+    const bool runLen = lane < cnt && pass1Len == kLongMatch && resDist == 1u && resLen > kSameLetter;
+    if (__ballot(runLen) && lane == 0) atomicOr(&longFlag[S.block], kFlagRun);
   }
 }
 
@@ -1709,7 +1715,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
       cDist = bDist;
       exact = true;
     }
-    if (rmqLen && lane == 0) atomicOr(&longFlag[S.block], 1u);
+    if (rmqLen && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
   };
 
   if (fixMode) {
@@ -2280,7 +2286,8 @@ void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint3
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
                                              Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount,
                                              uint32_t maxChain, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                             uint64_t matchBase, uint32_t* __restrict__ sel, int* __restrict__ status)
+                                             uint64_t matchBase, uint32_t* __restrict__ sel, const uint32_t* __restrict__ longFlag,
+                                             int* __restrict__ status)
 {
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
@@ -2299,6 +2306,8 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, con
     for (uint64_t i = from + lane; i < n; i += 64) S[i] = 0;
   }
   if (maxChain > (uint32_t)kLazyMax || n < (uint64_t)kTailNoMatch) return;
+  // blocks without shortcut intervals or runs beyond MaxSameLetter: k_lazy_walk/fix/clear, in parallel
+  if (ivCount[blockIdx.x] == 0u && (longFlag[blockIdx.x] & kFlagRun) == 0u) return;
 
   // one lane replays the reference's loop over an LDS copy of each 64-position chunk
   __shared__ uint32_t chunkL[64];
@@ -2398,6 +2407,240 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, con
   }
 }
 
+// ================================================================================================
+// Greedy/lazy levels in parallel.  Without shortcut intervals and without distance-1 matches longer
+// than MaxSameLetter in the block (no same-letter shortcut can fire, smallz4.h:631-643), the
+// reference's bookkeeping (smallz4.h:726-744) touches only positions that have an exact predecessor
+// ("linked": a match of >= 4 bytes), and it is a chain of searched positions that alternates:
+//   fresh search at q (skip was 0)  -> the next linked position is searched too (lazy evaluation);
+//   lazy search at q                -> the next L(q) linked positions are skipped, the one after is
+//                                      searched fresh.
+// Linked positions that are not searched keep length 0 (the reference never searched there).
+// k_lazy_walk walks this chain per 4096-position sub-segment from an assumed start (the
+// sub-segment's first linked position, fresh); k_lazy_fix walks the sub-segments of a block in order
+// and re-walks from the true entry until it meets the speculative walk at the same position in the
+// same mode (from there both are the same walk); k_lazy_clear zeroes the linked positions no walk
+// searched.  Other blocks keep k_prep's serial replay.
+// ================================================================================================
+constexpr int kWalkWaves = 4;         // sub-segments per k_walk / k_lazy_* workgroup
+constexpr uint32_t kLazyCap = 1400;   // searched positions per sub-segment: <= 2 per 6 linked + 2
+constexpr uint32_t kLazyEnd = 0x7FFFFFFFu;
+
+__device__ __forceinline__ bool lazy_fast_block(const uint32_t* ivCount, const uint32_t* longFlag, uint32_t b)
+{
+  return ivCount[b] == 0u && (longFlag[b] & kFlagRun) == 0u;
+}
+
+// index of the k-th set bit of m (0-based; k < popcount(m)), uniform
+__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t k)
+{
+  uint32_t base = 0;
+#pragma unroll
+  for (uint32_t w = 32; w >= 1; w >>= 1) {
+    const uint64_t lowMask = (w == 64) ? ~0ull : ((1ull << w) - 1ull);
+    const uint32_t c = (uint32_t)__popcll(m & lowMask);
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      base += w;
+    }
+  }
+  return base;
+}
+
+// the need-th (0-based) linked position at or after pos, reading 64 positions per step from HBM
+// (the repair walk: short); kLazyEnd when there is none up to lastSearch
+__device__ __forceinline__ uint32_t lazy_next_direct(const uint32_t* L, uint32_t pos, uint32_t need, uint32_t lastSearch)
+{
+  const uint32_t lane = lane_id();
+  while (pos <= lastSearch) {
+    const uint32_t x = pos + lane;
+    const uint64_t mask = __ballot(x <= lastSearch && L[x] >= (uint32_t)kMinMatch);
+    const uint32_t pc = (uint32_t)__popcll(mask);
+    if (need < pc) return pos + select64(mask, need);
+    need -= pc;
+    pos += 64;
+  }
+  return kLazyEnd;
+}
+
+__global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __restrict__ blocks,
+                                                               const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                               const uint32_t* __restrict__ ivCount,
+                                                               const uint32_t* __restrict__ longFlag,
+                                                               const uint32_t* __restrict__ mlen, uint64_t matchBase,
+                                                               uint32_t* __restrict__ slotsAll, uint4* __restrict__ state)
+{
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  if (!lazy_fast_block(ivCount, longFlag, ws.x)) return;
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t lastSearch = n - kTailNoMatch;  // inclusive
+  const uint32_t* L = mlen + (B.start - matchBase);
+  uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap) + kLazyCap;
+  const uint32_t a = ws.y * kWalkSeg;
+  const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+  // four 64-position windows of lengths in registers, loads three windows ahead (as k_walk)
+  auto ldw = [&](uint32_t b) -> uint32_t { return b + lane <= lastSearch ? L[b + lane] : 0u; };
+  uint32_t wbase = a & ~63u;
+  uint32_t wL = ldw(wbase), xL1 = ldw(wbase + 64), xL2 = ldw(wbase + 128), xL3 = ldw(wbase + 192);
+  uint32_t pos = a, need = 0, mode = 0, m = 0, q = kLazyEnd;  // mode 0: fresh, 1: lazy
+  while (true) {
+    // q = the need-th linked position at or after pos
+    q = kLazyEnd;
+    while (pos <= lastSearch) {
+      while (pos >= wbase + 64) {
+        if (pos < wbase + 256) {
+          wbase += 64;
+          wL = xL1;
+          xL1 = xL2;
+          xL2 = xL3;
+          xL3 = ldw(wbase + 192);
+        } else {
+          wbase = pos & ~63u;
+          wL = ldw(wbase);
+          xL1 = ldw(wbase + 64);
+          xL2 = ldw(wbase + 128);
+          xL3 = ldw(wbase + 192);
+        }
+      }
+      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch) & (~0ull << (pos - wbase));
+      const uint32_t pc = (uint32_t)__popcll(mask);
+      if (need < pc) {
+        q = wbase + select64(mask, need);
+        break;
+      }
+      need -= pc;
+      pos = wbase + 64;
+    }
+    if (q >= aNext) break;
+    if (m >= kLazyCap) {  // cannot happen (see kLazyCap); stop rather than overrun
+      q = kLazyEnd;
+      break;
+    }
+    if (lane == 0) slots[m] = q;
+    m++;
+    need = mode == 0 ? 0u : rdlane(wL, q - wbase);
+    mode ^= 1u;
+    pos = q + 1;
+  }
+  if (lane == 0) state[idx] = make_uint4(kLazyCap, kLazyCap + m, q | (mode << 31), 0u);
+}
+
+__global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ ivCount,
+                                                 const uint32_t* __restrict__ longFlag, const uint32_t* __restrict__ mlen,
+                                                 uint64_t matchBase, uint32_t* __restrict__ slotsAll,
+                                                 uint4* __restrict__ state, int* __restrict__ status)
+{
+  __shared__ uint32_t fix[kLazyCap];
+  if (!lazy_fast_block(ivCount, longFlag, blockIdx.x)) return;
+  const Block B = blocks[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t lastSearch = n - kTailNoMatch;
+  const uint32_t* L = mlen + (B.start - matchBase);
+  for (uint32_t k = 1; k < B.walkCount; k++) {
+    const uint32_t idx = B.walkFirst + k;
+    const uint32_t ex = state[idx - 1].z;  // exact exit of the sub-segment before: (position, mode)
+    const uint32_t entry = ex & 0x7FFFFFFFu, emode = ex >> 31;
+    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+    const uint4 st = state[idx];
+    uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
+    const uint32_t m = st.y - kLazyCap;
+    if (entry >= aNext) {
+      if (lane == 0) state[idx] = make_uint4(st.y, st.y, ex, 0u);  // nothing searched here
+      continue;
+    }
+    // first speculative entry at or after p (64 slots per step)
+    auto first_at = [&](uint32_t from, uint32_t p) -> uint32_t {
+      for (uint32_t b = from; b < m; b += 64) {
+        const uint64_t ge = __ballot(b + lane < m && slots[kLazyCap + b + lane] >= p);
+        if (ge) return b + (uint32_t)__builtin_ctzll(ge);
+      }
+      return m;
+    };
+    // the speculative walk searched p in mode md (its i-th search is in mode i & 1)
+    auto visited = [&](uint32_t i, uint32_t p, uint32_t md) -> bool {
+      return i < m && slots[kLazyCap + i] == p && (i & 1u) == md;
+    };
+    uint32_t i = first_at(0, entry);
+    if (visited(i, entry, emode)) {
+      if (lane == 0) state[idx] = make_uint4(kLazyCap + i, st.y, st.z, 0u);
+      continue;
+    }
+    // re-walk from the true entry until it meets the speculative walk
+    uint32_t q = entry, md = emode, f = 0;
+    bool merged = false;
+    while (q < aNext) {
+      if (f >= kLazyCap) {
+        if (lane == 0) atomicOr(status, kStInvariant);
+        break;
+      }
+      if (lane == 0) fix[f] = q;
+      f++;
+      const uint32_t need = md == 0 ? 0u : L[q];
+      md ^= 1u;
+      q = lazy_next_direct(L, q + 1, need, lastSearch);
+      if (q >= aNext) break;
+      i = first_at(i, q);
+      if (visited(i, q, md)) {
+        merged = true;
+        break;
+      }
+    }
+    __syncthreads();
+    const uint32_t iMerge = merged ? i : m;
+    const uint32_t start = kLazyCap + iMerge - f;
+    for (uint32_t t = lane; t < f; t += 64) slots[start + t] = fix[t];
+    if (lane == 0) state[idx] = make_uint4(start, st.y, merged ? st.z : (q | (md << 31)), 0u);
+    __syncthreads();
+  }
+}
+
+// the linked positions of a sub-segment that no walk searched get length 0
+__global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __restrict__ blocks,
+                                                                const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                                const uint32_t* __restrict__ ivCount,
+                                                                const uint32_t* __restrict__ longFlag,
+                                                                uint32_t* __restrict__ mlen, uint64_t matchBase,
+                                                                const uint32_t* __restrict__ slotsAll,
+                                                                const uint4* __restrict__ state)
+{
+  __shared__ uint32_t bits[kWalkWaves][kWalkSeg / 32];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  if (!lazy_fast_block(ivCount, longFlag, ws.x)) return;
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t lastSearch = n - kTailNoMatch;
+  uint32_t* L = mlen + (B.start - matchBase);
+  const uint32_t a = ws.y * kWalkSeg;
+  const uint32_t hi = a + kWalkSeg - 1 < lastSearch ? a + kWalkSeg - 1 : lastSearch;  // inclusive
+  if (a > hi) return;
+  uint32_t* bw = bits[wave];
+  for (uint32_t t = lane; t < kWalkSeg / 32; t += 64) bw[t] = 0;
+  const uint4 st = state[idx];
+  const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
+  for (uint32_t t = st.x + lane; t < st.y; t += 64) {
+    const uint32_t q = slots[t] - a;
+    atomicOr(&bw[q >> 5], 1u << (q & 31));
+  }
+  for (uint32_t x0 = a; x0 <= hi; x0 += 64) {
+    const uint32_t x = x0 + lane;
+    if (x <= hi && L[x] >= (uint32_t)kMinMatch && !((bw[(x - a) >> 5] >> ((x - a) & 31)) & 1u)) L[x] = 0;
+  }
+}
+
 constexpr int kSpecWaves = 4;  // independent segments per workgroup (workgroup slots, not LDS, bound occupancy)
 
 template <bool kRmq>
@@ -2428,7 +2671,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   const int32_t top = (int32_t)(B.end - B.start) - 1 - kTailLiterals;
   // blocks with matches of kRmqLen+ run in the kRmq instantiation (range minima, carried chains);
   // the others in the lean one
-  const bool rmq = longFlag[G.block] != 0u;
+  const bool rmq = (longFlag[G.block] & kFlagRmq) != 0u;
   if (rmq != kRmq) return;
   uint32_t* up = upAll + base;
   uint32_t* down = downAll + base;
@@ -2718,7 +2961,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   uint32_t* S = sel + base;
   const uint32_t first = dpSegs[B.dpFirst].hi;  // n - 6: the last parsed position
   const int32_t top = (int32_t)first;
-  const bool rmq = longFlag[blockIdx.x] != 0u;
+  const bool rmq = (longFlag[blockIdx.x] & kFlagRmq) != 0u;
   uint32_t* up = upAll + base;
   uint32_t* down = downAll + base;
   if (lane == 0) {
@@ -2983,7 +3226,6 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
 // was wrong (k_walk_fix), and turned into 16-byte tokens (literal run, match) by k_seg_tokens.
 // ================================================================================================
 
-constexpr int kWalkWaves = 4;  // sub-segments per k_walk workgroup
 
 // k_walk: one wavefront per sub-segment walks the parse forward from the sub-segment's first
 // position as if a sequence started there, and records the positions of the matches it takes
@@ -3501,12 +3743,28 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
 }
 
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
-                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, int* status, hipStream_t s)
+                 uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, const uint32_t* longFlag, int* status,
+                 hipStream_t s)
 {
   if (nblocks)
     hipLaunchKernelGGL(k_prep, dim3(nblocks), dim3(64), 0, s, in, blocks, iv, ivCount, maxChain, mlen, mdist, matchBase, sel,
-                       status);
+                       longFlag, status);
 }
+
+void launch_lazy(const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk, const uint32_t* ivCount,
+                 const uint32_t* longFlag, uint32_t* mlen, uint64_t matchBase, uint32_t* slots, uint4* state, int* status,
+                 hipStream_t s)
+{
+  if (!nblocks || !nwalk) return;
+  const uint32_t grid = (nwalk + kWalkWaves - 1) / kWalkWaves;
+  hipLaunchKernelGGL(k_lazy_walk, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, ivCount, longFlag, mlen,
+                     matchBase, slots, state);
+  hipLaunchKernelGGL(k_lazy_fix, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, longFlag, mlen, matchBase, slots, state, status);
+  hipLaunchKernelGGL(k_lazy_clear, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, ivCount, longFlag, mlen,
+                     matchBase, slots, state);
+}
+
+uint32_t lazy_slots_per_walk() { return 2 * kLazyCap; }
 
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
