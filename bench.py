@@ -71,6 +71,11 @@ WORKLOADS = {
     "silesia": ("configs[2]", "synthetic Silesia-shaped mixed content (synth.silesia_like; the corpus is not available offline)",
                 4 << 20, lambda world: 211_938_580,
                 lambda lo, hi: synth.silesia_like(hi, seed=2)[lo:hi]),
+    # diagnostic shapes (not BASELINE configs): the kernels' floors on incompressible / all-run data
+    "random": ("diagnostic", "synthetic: urandom bytes (numpy, seeded)", 65536, lambda world: 100_000_000,
+               lambda lo, hi: synth.random_bytes(hi, seed=8)[lo:hi]),
+    "zeros": ("diagnostic", "synthetic: all zero bytes", 65536, lambda world: 100_000_000,
+              lambda lo, hi: bytes(hi - lo)),
 }
 
 

@@ -7,8 +7,8 @@ Writes
   <tag>_kernel_stats.csv   the rocprofv3 --kernel-trace --stats table, as collected
   <tag>_kernel_stats.md    per kernel: calls, average duration, share, and the PMC passes
                            (FETCH_SIZE x2, WRITE_SIZE, SQ issue counters) averaged per launch
-  <tag>_find_hbm_bytes.json  k_find_sorted's HBM bytes per launch (bench.py reads this file
-                           for the roofline "traffic" field)
+  <tag>_pmc.json           k_find_sorted's HBM bytes per launch and its issue rates (bench.py reads
+                           the newest one whose "config" matches its workload for the roofline)
   <tag>_bench.json         the bench.py JSON line of the same run
 
 FETCH_SIZE is doubled (MI355X_MICROARCH.md, HBM: gfx950 tallies 128-B requests at 64 B);
@@ -97,24 +97,29 @@ def main():
                      f"{fmt(fe, 2 * 1024 / 1e6)} | {fmt(wr, 1024 / 1e6)} | {fmt(valu, 'e')} | {fmt(salu, 'e')} | "
                      f"{fmt(lds, 'e')} | {fmt(wait, 1.0, 0)} |")
         if k.startswith("sz4::k_find_sorted"):
-            find = (k, float(r["AverageNs"]), fe, wr)
+            find = (k, float(r["AverageNs"]), fe, wr, valu, salu)
     with open(os.path.join(HERE, f"{a.tag}_kernel_stats.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
     bench = os.path.join(src, "bench.json")
     if os.path.exists(bench):
         shutil.copy(bench, os.path.join(HERE, f"{a.tag}_bench.json"))
     if find:
-        k, avg_ns, fe, wr = find
+        k, avg_ns, fe, wr, valu, salu = find
         fb = None if fe is None else int(round(fe * 1024 * 2))
         wb = None if wr is None else int(round(wr * 1024))
+        cycles = avg_ns * 1e-9 * 2.4e9  # MI355X_MICROARCH.md: 2.4 GHz
         out = {"kernel": "k_find_sorted", "tag": a.tag,
-               "workload": "bench.py default: 100 MB enwik8-shaped, 64 KiB blocks, -9",
+               "config": {"workload": "enwik8", "bytes_per_gpu": 100_000_000, "block_size": 65536, "level": 9},
                "avg_duration_us": round(avg_ns / 1e3, 1),
                "fetch_bytes_corrected": fb, "write_bytes": wb,
                "hbm_bytes_per_launch": None if fb is None or wb is None else fb + wb,
-               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (profiles/collect.sh); "
-                         "FETCH_SIZE doubled per MI355X_MICROARCH.md; WRITE_SIZE as reported"}
-        with open(os.path.join(HERE, f"{a.tag}_find_hbm_bytes.json"), "w") as f:
+               "valu_per_simd_cycle": None if valu is None else round(valu / (cycles * 1024), 4),
+               "salu_per_cu_cycle": None if salu is None else round(salu / (cycles * 256), 4),
+               "method": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass, each a separate run "
+                         "(profiles/collect.sh); FETCH_SIZE doubled per MI355X_MICROARCH.md; WRITE_SIZE as reported; "
+                         "issue rates = SQ_INSTS_VALU / (duration x 2.4 GHz x 1024 SIMDs), "
+                         "SQ_INSTS_SALU / (duration x 2.4 GHz x 256 CUs)"}
+        with open(os.path.join(HERE, f"{a.tag}_pmc.json"), "w") as f:
             json.dump(out, f, indent=1)
             f.write("\n")
     print("\n".join(lines))

@@ -2448,21 +2448,51 @@ __device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t k)
   return base;
 }
 
-// the need-th (0-based) linked position at or after pos, reading 64 positions per step from HBM
-// (the repair walk: short); kLazyEnd when there is none up to lastSearch
-__device__ __forceinline__ uint32_t lazy_next_direct(const uint32_t* L, uint32_t pos, uint32_t need, uint32_t lastSearch)
-{
-  const uint32_t lane = lane_id();
-  while (pos <= lastSearch) {
-    const uint32_t x = pos + lane;
-    const uint64_t mask = __ballot(x <= lastSearch && L[x] >= (uint32_t)kMinMatch);
-    const uint32_t pc = (uint32_t)__popcll(mask);
-    if (need < pc) return pos + select64(mask, need);
-    need -= pc;
-    pos += 64;
+// the searched-position chain over a register window of lengths: four 64-position windows in
+// registers, loads three windows ahead (as k_walk); wave-uniform state
+struct LazyWalker {
+  const uint32_t* L;
+  uint32_t lastSearch;  // inclusive
+  uint32_t wbase, wL, xL1, xL2, xL3;
+  __device__ __forceinline__ uint32_t ldw(uint32_t b) const
+  {
+    const uint32_t lane = lane_id();
+    return b + lane <= lastSearch ? L[b + lane] : 0u;
   }
-  return kLazyEnd;
-}
+  __device__ __forceinline__ void start(uint32_t pos)
+  {
+    wbase = pos & ~63u;
+    wL = ldw(wbase);
+    xL1 = ldw(wbase + 64);
+    xL2 = ldw(wbase + 128);
+    xL3 = ldw(wbase + 192);
+  }
+  // the need-th (0-based) linked position at or after pos, kLazyEnd when there is none
+  __device__ __forceinline__ uint32_t next(uint32_t pos, uint32_t need)
+  {
+    while (pos <= lastSearch) {
+      while (pos >= wbase + 64) {
+        if (pos < wbase + 256) {
+          wbase += 64;
+          wL = xL1;
+          xL1 = xL2;
+          xL2 = xL3;
+          xL3 = ldw(wbase + 192);
+        } else {
+          start(pos);
+        }
+      }
+      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch) & (~0ull << (pos - wbase));
+      const uint32_t pc = (uint32_t)__popcll(mask);
+      if (need < pc) return wbase + select64(mask, need);
+      need -= pc;
+      pos = wbase + 64;
+    }
+    return kLazyEnd;
+  }
+  // length at q (q inside the current window: the position next() just returned)
+  __device__ __forceinline__ uint32_t len(uint32_t q) const { return rdlane(wL, q - wbase); }
+};
 
 __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __restrict__ blocks,
                                                                const uint2* __restrict__ walkSegs, uint32_t nwalk,
@@ -2480,44 +2510,16 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   const Block B = blocks[ws.x];
   const uint32_t n = (uint32_t)(B.end - B.start);
   if (n < (uint32_t)kTailNoMatch) return;
-  const uint32_t lastSearch = n - kTailNoMatch;  // inclusive
-  const uint32_t* L = mlen + (B.start - matchBase);
   uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap) + kLazyCap;
   const uint32_t a = ws.y * kWalkSeg;
   const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
-  // four 64-position windows of lengths in registers, loads three windows ahead (as k_walk)
-  auto ldw = [&](uint32_t b) -> uint32_t { return b + lane <= lastSearch ? L[b + lane] : 0u; };
-  uint32_t wbase = a & ~63u;
-  uint32_t wL = ldw(wbase), xL1 = ldw(wbase + 64), xL2 = ldw(wbase + 128), xL3 = ldw(wbase + 192);
-  uint32_t pos = a, need = 0, mode = 0, m = 0, q = kLazyEnd;  // mode 0: fresh, 1: lazy
+  LazyWalker w;
+  w.L = mlen + (B.start - matchBase);
+  w.lastSearch = n - kTailNoMatch;
+  w.start(a);
+  uint32_t pos = a, need = 0, mode = 0, m = 0, q;  // mode 0: fresh, 1: lazy
   while (true) {
-    // q = the need-th linked position at or after pos
-    q = kLazyEnd;
-    while (pos <= lastSearch) {
-      while (pos >= wbase + 64) {
-        if (pos < wbase + 256) {
-          wbase += 64;
-          wL = xL1;
-          xL1 = xL2;
-          xL2 = xL3;
-          xL3 = ldw(wbase + 192);
-        } else {
-          wbase = pos & ~63u;
-          wL = ldw(wbase);
-          xL1 = ldw(wbase + 64);
-          xL2 = ldw(wbase + 128);
-          xL3 = ldw(wbase + 192);
-        }
-      }
-      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch) & (~0ull << (pos - wbase));
-      const uint32_t pc = (uint32_t)__popcll(mask);
-      if (need < pc) {
-        q = wbase + select64(mask, need);
-        break;
-      }
-      need -= pc;
-      pos = wbase + 64;
-    }
+    q = w.next(pos, need);
     if (q >= aNext) break;
     if (m >= kLazyCap) {  // cannot happen (see kLazyCap); stop rather than overrun
       q = kLazyEnd;
@@ -2525,7 +2527,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
     }
     if (lane == 0) slots[m] = q;
     m++;
-    need = mode == 0 ? 0u : rdlane(wL, q - wbase);
+    need = mode == 0 ? 0u : w.len(q);
     mode ^= 1u;
     pos = q + 1;
   }
@@ -2537,46 +2539,56 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
                                                  uint64_t matchBase, uint32_t* __restrict__ slotsAll,
                                                  uint4* __restrict__ state, int* __restrict__ status)
 {
-  __shared__ uint32_t fix[kLazyCap];
+  __shared__ uint32_t spec[kLazyCap];  // the sub-segment's speculative searches
+  __shared__ uint32_t fix[kLazyCap];   // the repaired ones in front of them
   if (!lazy_fast_block(ivCount, longFlag, blockIdx.x)) return;
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = (uint32_t)(B.end - B.start);
-  if (n < (uint32_t)kTailNoMatch) return;
-  const uint32_t lastSearch = n - kTailNoMatch;
-  const uint32_t* L = mlen + (B.start - matchBase);
+  if (n < (uint32_t)kTailNoMatch || B.walkCount < 2) return;
+  LazyWalker w;
+  w.L = mlen + (B.start - matchBase);
+  w.lastSearch = n - kTailNoMatch;
+  w.wbase = 0xFFFFFFC0u;  // no window loaded yet
+  uint32_t ex = state[B.walkFirst].z;  // exact exit of sub-segment 0 (walked from the block start)
+  uint4 st = state[B.walkFirst + 1];
   for (uint32_t k = 1; k < B.walkCount; k++) {
     const uint32_t idx = B.walkFirst + k;
-    const uint32_t ex = state[idx - 1].z;  // exact exit of the sub-segment before: (position, mode)
+    const uint4 stNext = k + 1 < B.walkCount ? state[idx + 1] : make_uint4(0, 0, 0, 0);  // one ahead
     const uint32_t entry = ex & 0x7FFFFFFFu, emode = ex >> 31;
     const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
-    const uint4 st = state[idx];
     uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
     const uint32_t m = st.y - kLazyCap;
     if (entry >= aNext) {
       if (lane == 0) state[idx] = make_uint4(st.y, st.y, ex, 0u);  // nothing searched here
-      continue;
+      st = stNext;
+      continue;  // ex unchanged: the entry of the next sub-segment
     }
-    // first speculative entry at or after p (64 slots per step)
+    for (uint32_t t = lane; t < m; t += 64) spec[t] = slots[kLazyCap + t];
+    __syncthreads();
+    // first speculative entry at or after p (64 slots per step); the speculative walk's i-th search
+    // is in mode i & 1
     auto first_at = [&](uint32_t from, uint32_t p) -> uint32_t {
       for (uint32_t b = from; b < m; b += 64) {
-        const uint64_t ge = __ballot(b + lane < m && slots[kLazyCap + b + lane] >= p);
+        const uint64_t ge = __ballot(b + lane < m && spec[b + lane] >= p);
         if (ge) return b + (uint32_t)__builtin_ctzll(ge);
       }
       return m;
     };
-    // the speculative walk searched p in mode md (its i-th search is in mode i & 1)
-    auto visited = [&](uint32_t i, uint32_t p, uint32_t md) -> bool {
-      return i < m && slots[kLazyCap + i] == p && (i & 1u) == md;
-    };
+    auto visited = [&](uint32_t i, uint32_t p, uint32_t md) -> bool { return i < m && spec[i] == p && (i & 1u) == md; };
     uint32_t i = first_at(0, entry);
     if (visited(i, entry, emode)) {
       if (lane == 0) state[idx] = make_uint4(kLazyCap + i, st.y, st.z, 0u);
+      ex = st.z;
+      st = stNext;
+      __syncthreads();
       continue;
     }
     // re-walk from the true entry until it meets the speculative walk
     uint32_t q = entry, md = emode, f = 0;
     bool merged = false;
+    if (w.wbase == 0xFFFFFFC0u || q < w.wbase || q >= w.wbase + 256) w.start(q);
+    (void)w.next(q, 0);  // q is linked: brings its window in
     while (q < aNext) {
       if (f >= kLazyCap) {
         if (lane == 0) atomicOr(status, kStInvariant);
@@ -2584,9 +2596,9 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
       }
       if (lane == 0) fix[f] = q;
       f++;
-      const uint32_t need = md == 0 ? 0u : L[q];
+      const uint32_t need = md == 0 ? 0u : w.len(q);
       md ^= 1u;
-      q = lazy_next_direct(L, q + 1, need, lastSearch);
+      q = w.next(q + 1, need);
       if (q >= aNext) break;
       i = first_at(i, q);
       if (visited(i, q, md)) {
@@ -2598,7 +2610,9 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
     const uint32_t iMerge = merged ? i : m;
     const uint32_t start = kLazyCap + iMerge - f;
     for (uint32_t t = lane; t < f; t += 64) slots[start + t] = fix[t];
-    if (lane == 0) state[idx] = make_uint4(start, st.y, merged ? st.z : (q | (md << 31)), 0u);
+    ex = merged ? st.z : (q | (md << 31));
+    if (lane == 0) state[idx] = make_uint4(start, st.y, ex, 0u);
+    st = stNext;
     __syncthreads();
   }
 }
