@@ -20,6 +20,7 @@
 // reproduce are restated in DESIGN.md section 3.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <type_traits>
 
@@ -968,7 +969,9 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       const uint32_t sb = satBest[lane];
       bestKey = sb > bestKey ? sb : bestKey;
       const uint32_t bl = bestKey >> 17;
-      if (bl >= 4u) {
+      // a big target stays handed on: the below-chunk loop lets every lane take its candidates (no
+      // window test), so it may hold a partial maximum here
+      if (bl >= 4u && !big) {
         bestLen = bl;
         bestDist = (uint32_t)(p - (S.w0 + slot_pos(compact, small, bestKey & 0x1FFFFu)));
         isLong = bl >= limit && limit < room;
@@ -1791,6 +1794,319 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
       }
       walk_stretch(q, cLen, cDist, exact);
     }
+  }
+}
+
+// ================================================================================================
+// k_find_big (-9, between pass 1 and pass 2): the targets pass 1 handed on because their key group
+// holds more than kBigGroup candidates (structured records, tables, padding).  Walking such a group
+// once per target is quadratic; instead the maximum is split (the longest-previous-factor identity):
+//   best(p) = better of  LM(p)                  -- over the LEFT-MAXIMAL candidates c of p only:
+//                                                  data[c-1] != data[p-1], or c-1 not a chain position
+//            and         (L(p-1) - 1, D(p-1))    -- every other candidate c has c-1 as a candidate of
+//                                                  p-1 with one byte more in common, and the nearest of
+//                                                  the longest of those is p-1's own result
+// ("better": longer, then nearer -- the reference's strict-improvement walk, smallz4.h:190-252).
+// Unrolled along the text this is a prefix maximum of  key(q) = (q + len(q)) << 16 | (0xFFFF - dist(q))
+// from the last target whose result is already exact (pass 1), and it needs LM(p) only.
+//   1. the segment's big groups are regrouped by the candidates' preceding byte (class 256: no
+//      predecessor), so a wavefront of 64 targets of one class scans every candidate EXCEPT its own
+//      class in one broadcast pass (mixed-class wavefronts scan all and filter per lane);
+//   2. LM(p) -> lm[p] (specLen, free until pass 2);
+//   3. the prefix maximum in text order (16 wavefronts, carries through LDS) resolves every big target
+//      that follows an exact target of this segment; the rest (a segment start inside a run of big
+//      targets, a result at the pass-1 cap) stay marked for pass 2.
+// Only blocks without a lookback cut or shortcut intervals (independent blocks): the identity needs
+// every candidate position to be a chain position.
+// ================================================================================================
+constexpr uint32_t kMaxBigGroups = 16;  // > 128 Ki window slots / kBigGroup
+constexpr uint32_t kClsNone = 256;      // preceding byte class of a position without a chain predecessor
+
+template <bool kLds>
+__global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                                           const Block* __restrict__ blocks,
+                                                           const uint32_t* __restrict__ ivCount,
+                                                           const uint2* __restrict__ compactAll, uint2* __restrict__ scratchAll,
+                                                           uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
+                                                           uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                           uint64_t matchBase, uint32_t* __restrict__ lm)
+{
+  extern __shared__ __attribute__((aligned(16))) uint32_t win[];
+  __shared__ uint32_t s_groups[2 * kMaxBigGroups];
+  __shared__ uint32_t s_ng, s_next;
+  __shared__ uint32_t s_cls[kClsNone + 2], s_tcls[kClsNone + 2];  // class starts (candidates, targets)
+  __shared__ uint32_t s_cur[2][kClsNone + 1];                      // scatter cursors
+  __shared__ uint32_t s_chunk[kClsNone + 2];                       // first chunk of each class
+  __shared__ uint32_t s_hasHead[kFindThreads / 64], s_outValid[kFindThreads / 64];
+  __shared__ uint64_t s_outKey[kFindThreads / 64];
+  const Segment S = segs[blockIdx.x];
+  const Block B = blocks[S.block];
+  if (!segLong[blockIdx.x] || B.cut != kNone || ivCount[S.block] != 0u || (B.prev != kNoBlock && ivCount[B.prev] != 0u))
+    return;  // uniform over the workgroup
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  const void* compact = compactAll + S.elemOff;
+  const uint32_t E = (uint32_t)(S.s1 - S.w0);  // no intervals: every window position is a slot
+  const bool small = compact_small(S);
+
+  // 1. big groups: last slot s of a group with s - gs > kBigGroup
+  if (tid == 0) s_ng = 0;
+  __syncthreads();
+  for (uint32_t s = tid; s < E; s += kFindThreads) {
+    const uint32_t g = slot_gs(compact, small, E, s);
+    if (s - g > kBigGroup && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g)) {
+      const uint32_t k = atomicAdd(&s_ng, 1u);
+      if (k < kMaxBigGroups) {
+        s_groups[2 * k] = g;
+        s_groups[2 * k + 1] = s + 1;
+      }
+    }
+  }
+  __syncthreads();
+  const uint32_t ng = s_ng;
+  if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
+
+  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
+  {
+    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
+    const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
+    src.w = win;
+    src.base = S.w0;
+    if constexpr (!kLds) {
+      src.lim = S.w0 + 4ull * words;
+      src.in = in;
+    }
+  }
+  const uint64_t stopAbs = B.end - kTailLiterals;
+  const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
+  // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
+  auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
+  uint32_t* C = reinterpret_cast<uint32_t*>(scratchAll + S.elemOff);  // candidates: cls << 17 | rel
+  uint32_t* T = C + E;                                                 // targets: rel
+  __syncthreads();
+
+  for (uint32_t gi = 0; gi < ng; gi++) {
+    const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
+    for (uint32_t k = tid; k < 2 * (kClsNone + 1); k += kFindThreads) (&s_cur[0][0])[k] = 0;
+    __syncthreads();
+    // counts per class (candidates: the whole group; targets: pass 1's big ones)
+    for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
+      const uint32_t r = slot_pos(compact, small, s);
+      const uint64_t q = S.w0 + r;
+      const uint32_t c = cls_of(q);
+      atomicAdd(&s_cur[0][c], 1u);
+      if (s - ga > kBigGroup && q >= S.s0) atomicAdd(&s_cur[1][c], 1u);
+    }
+    __syncthreads();
+    if (tid < 2) {
+      uint32_t* st = tid == 0 ? s_cls : s_tcls;
+      uint32_t acc = 0, chunks = 0;
+      for (uint32_t k = 0; k <= kClsNone; k++) {
+        const uint32_t n = s_cur[tid][k];
+        st[k] = acc;
+        s_cur[tid][k] = acc;
+        if (tid == 1) {
+          s_chunk[k] = chunks;
+          chunks += (n + 63) / 64;
+        }
+        acc += n;
+      }
+      st[kClsNone + 1] = acc;
+      if (tid == 1) {
+        s_chunk[kClsNone + 1] = chunks;
+        s_next = 0;
+      }
+    }
+    __syncthreads();
+    for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
+      const uint32_t r = slot_pos(compact, small, s);
+      const uint64_t q = S.w0 + r;
+      const uint32_t c = cls_of(q);
+      C[ga + atomicAdd(&s_cur[0][c], 1u)] = (c << 17) | r;
+      if (s - ga > kBigGroup && q >= S.s0) T[ga + atomicAdd(&s_cur[1][c], 1u)] = r;
+    }
+    __threadfence_block();
+    __syncthreads();
+
+    // 2. LM of every big target: chunks of up to 64 targets, taken class by class; a class's last,
+    //    partial chunk is filled up with the next classes' first targets (mixed: scan all, filter)
+    const uint32_t nT = s_tcls[kClsNone + 1];
+    const uint32_t nChunks = (nT + 63) / 64;
+    while (true) {
+      uint32_t item = 0;
+      if (lane == 0) item = atomicAdd(&s_next, 1u);
+      item = rdlane(item, 0);
+      if (item >= nChunks) break;
+      const uint32_t t = item * 64 + lane;
+      const bool act = t < nT;
+      const uint32_t pRel = act ? T[ga + t] : 0u;
+      const uint64_t p = S.w0 + pRel;
+      const uint32_t myCls = act ? cls_of(p) : kClsNone + 1;
+      // p's own class is excluded only when p-1 is a target of this block (its result carries to p)
+      const uint32_t exCls = act && p > B.start && myCls < kClsNone ? myCls : kClsNone + 1;
+      const uint32_t me0 = act ? src.ld4(p) : 0u, me1 = act ? src.ld4(p + 4) : 0u, me2 = act ? src.ld4(p + 8) : 0u;
+      const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
+      const uint32_t limit = room < kLongCap9 ? room : kLongCap9;
+      const uint32_t cap12 = limit < 12u ? limit : 12u;
+      const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
+      // candidate ranges of C: one class for the whole wavefront -> skip it; else scan everything
+      const uint32_t e0 = rdlane(exCls, 0);
+      const bool one = __ballot(act && exCls != e0) == 0 && e0 < kClsNone;
+      uint32_t r0a = ga, r0b = gb, r1a = gb, r1b = gb;
+      if (one) {
+        r0b = ga + s_cls[e0];
+        r1a = ga + s_cls[e0 + 1];
+      }
+      uint32_t bestKey = 0;
+      for (int part = 0; part < 2; part++) {
+        const uint32_t lo = part == 0 ? r0a : r1a, hi = part == 0 ? r0b : r1b;
+        for (uint32_t base = lo; base < hi; base += 64) {
+          const uint32_t ci = base + lane;
+          const uint32_t ce = ci < hi ? C[ci] : 0xFFFFFFFFu;
+          const uint32_t cr = ce & 0x1FFFFu;
+          const uint64_t cp = S.w0 + (ci < hi ? cr : 0u);
+          const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
+          const uint32_t n = hi - base < 64u ? hi - base : 64u;
+          for (uint32_t j = 0; j < n; j++) {
+            const uint32_t ej = rdlane(ce, j), k0 = rdlane(f0, j), k1 = rdlane(f1, j), k2 = rdlane(f2, j);
+            const uint32_t c = ej & 0x1FFFFu;
+            const bool ok = act && c < pRel && c >= lbRel && (ej >> 17) != exCls && k0 == me0;
+            const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
+            const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+            const uint32_t z = min(z1, 32u + min(z2, 32u));
+            uint32_t lcp = min(4u + (z >> 3), cap12);
+            if (ok && lcp == 12u && limit > 12u) {
+              // both share 12 bytes: the exact prefix, unless the 4 bytes ending at the current best
+              // length already differ (then it stays below the best and cannot win)
+              const uint64_t cc = S.w0 + c;
+              const uint32_t bl = bestKey >> 17;
+              bool open = !(bl > 12u && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
+              while (open && lcp < limit) {
+                const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
+                if (x) {
+                  lcp += (uint32_t)__builtin_ctz(x) >> 3;
+                  open = false;
+                } else {
+                  lcp += 4;
+                }
+              }
+              if (lcp > limit) lcp = limit;
+            }
+            const uint32_t key = ok ? (lcp << 17) | c : 0u;
+            bestKey = key > bestKey ? key : bestKey;
+          }
+        }
+      }
+      if (act) {
+        const uint32_t bl = bestKey >> 17;
+        lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (uint32_t)(pRel - (bestKey & 0x1FFFFu)) : 0u;
+      }
+    }
+    __syncthreads();
+  }
+  __threadfence_block();
+  __syncthreads();
+
+  // 3. prefix maximum in text order.  Per target: E (exact: pass 1 finished it) resets the state to
+  //    its own key, U (unknown: a pass-1 long match, or LM at the cap) invalidates it, B (big) takes
+  //    the maximum of the state and its LM.  16 wavefronts take consecutive ranges; a range's carry-in
+  //    comes from the ranges before it (phase 0 summarises, phase 1 resolves).
+  const uint32_t nTg = (uint32_t)(S.s1 - S.s0);
+  const uint32_t waves = kFindThreads / 64;
+  const uint32_t span = ((nTg + waves - 1) / waves + 63) / 64 * 64;
+  const uint32_t r0 = wave * span, r1 = r0 + span < nTg ? r0 + span : nTg;
+  auto classify = [&](uint32_t i, uint32_t& kind, uint64_t& key) {
+    // kind 0 = B, 1 = E, 2 = U
+    const uint64_t p = S.s0 + i, idx = p - matchBase;
+    const uint32_t ml = mlen[idx], md = mdist[idx];
+    key = 0;
+    if (ml != kLongMatch) {
+      kind = 1;
+      if (ml >= (uint32_t)kMinMatch) key = ((uint64_t)(i + ml) << 16) | (0xFFFFu - md);
+      return;
+    }
+    const bool bit = (longBits[idx >> 5] >> (idx & 31)) & 1u;
+    if (!bit || md != 0u) {
+      kind = 2;
+      return;
+    }
+    const uint32_t v = lm[idx];
+    const uint32_t vl = v >> 16;
+    const uint32_t room = (uint32_t)(stopAbs - p);
+    if (vl >= kLongCap9 && room > kLongCap9) {
+      kind = 2;
+      return;
+    }
+    kind = 0;
+    if (vl >= (uint32_t)kMinMatch) key = ((uint64_t)(i + vl) << 16) | (0xFFFFu - (v & 0xFFFFu));
+  };
+  // inclusive segmented scan over the wavefront; returns (head seen, valid, key) per lane
+  auto scan = [&](uint32_t kind, uint64_t key, bool inRange, bool& head, bool& valid) -> uint64_t {
+    head = inRange && kind != 0u;
+    valid = kind == 1u;
+    uint64_t v = inRange ? key : 0ull;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint64_t vo = __shfl_up(v, d, 64);
+      const bool ho = __shfl_up((int)head, d, 64) != 0, va = __shfl_up((int)valid, d, 64) != 0;
+      if (lane >= (uint32_t)d && !head) {
+        v = vo > v ? vo : v;
+        valid = va;
+        head = ho;
+      }
+    }
+    return v;
+  };
+  for (int phase = 0; phase < 2; phase++) {
+    bool cValid = false;
+    uint64_t cKey = 0;
+    if (phase == 1) {
+      // carry-in: the block's first target has no predecessor (exact state, nothing to carry)
+      cValid = S.s0 == B.start;
+      for (uint32_t w = 0; w < wave; w++) {
+        if (s_hasHead[w]) {
+          cValid = s_outValid[w] != 0u;
+          cKey = s_outKey[w];
+        } else {
+          cKey = s_outKey[w] > cKey ? s_outKey[w] : cKey;
+        }
+      }
+    }
+    bool anyHead = false;
+    for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool inR = i < r1;
+      uint32_t kind = 2;
+      uint64_t key = 0;
+      if (inR) classify(i, kind, key);
+      bool head, valid;
+      uint64_t v = scan(kind, key, inR, head, valid);
+      if (!head) {
+        v = cKey > v ? cKey : v;
+        valid = cValid;
+      }
+      anyHead |= __ballot(inR && kind != 0u) != 0;
+      if (phase == 1 && inR && kind == 0u && valid) {
+        const uint64_t p = S.s0 + i, idx = p - matchBase;
+        const uint32_t len = (uint32_t)(v >> 16) > i ? (uint32_t)(v >> 16) - i : 0u;
+        const bool m = v != 0ull && len >= (uint32_t)kMinMatch;
+        mlen[idx] = m ? len : 0u;
+        mdist[idx] = m ? (uint16_t)(0xFFFFu - (uint32_t)(v & 0xFFFFu)) : (uint16_t)0;
+        atomicAnd(&longBits[idx >> 5], ~(1u << (idx & 31)));
+      }
+      // carry to the next 64: the last lane in range
+      const uint32_t last = (r1 - i0 < 64u ? r1 - i0 : 64u) - 1u;
+      cKey = ((uint64_t)rdlane((uint32_t)(v >> 32), last) << 32) | rdlane((uint32_t)v, last);
+      cValid = rdlane(valid ? 1u : 0u, last) != 0u;
+    }
+    if (phase == 0 && lane == 0) {
+      // summary with carry-in "nothing": valid/key after the range, or (no head) the max of its B keys
+      s_hasHead[wave] = anyHead ? 1u : 0u;
+      s_outValid[wave] = cValid ? 1u : 0u;
+      s_outKey[wave] = cKey;
+    }
+    __syncthreads();
   }
 }
 
@@ -2795,8 +3111,57 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
       const uint32_t mE = chain.costE + kMarginBias;
       chain.margin = mE < chain.margin ? mE : chain.margin;
       win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((63u - lane) << 2), (int)mcBuf) << 6;
-    } else
-    for (uint32_t t = 0; t < 64; t += 4) {
+    } else {
+    // a whole chunk whose match lengths are all <= 64: its batches unrolled (lane indices become
+    // immediates, no per-batch bounds), as long as no literal-length bump is reachable; the first batch
+    // that could reach one continues in the general loop below
+    uint32_t tFast = 0;
+    if (cnt == 64u) {
+      const uint32_t rowMax = row_max(myL);
+      const uint32_t cmax = max(max(rdlane(rowMax, 0), rdlane(rowMax, 16)), max(rdlane(rowMax, 32), rdlane(rowMax, 48)));
+      auto fast = [&](auto smallTag) -> uint32_t {
+        constexpr bool kSmall = decltype(smallTag)::value;  // every length <= 16: row 0 holds every candidate
+#pragma unroll
+        for (uint32_t t = 0; t < 64; t += 4) {
+          if (lits + 4u >= litBump) return t;
+          uint32_t nwin = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 4u) << 2), (int)win);
+          uint32_t kv[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const uint32_t Lr = rdlane(myL, t + (uint32_t)r);
+            kv[r] = lane + 1u + (uint32_t)r <= Lr ? win + kLen[r] : 0xFFFFFFFFu;
+          }
+          if constexpr (kSmall) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) kv[r] = rdlane(row_min(kv[r]), 0);
+          } else {
+            wave_min4(kv);
+          }
+          uint32_t mcost[4];
+          const uint32_t lits0 = lits;
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            // a match wins ties; invalid keys decode to costs no literal path reaches
+            const uint32_t mc = kv[r] >> 6;
+            const uint32_t c = min(costNext + 1u, mc);
+            lits = c == mc ? 0u : lits + 1u;
+            costNext = c;
+            mcost[r] = c;
+            kvBuf = wrlane(kvBuf, kv[r], t + (uint32_t)r);
+            mcBuf = wrlane(mcBuf, c, t + (uint32_t)r);
+          }
+          litBump = lits != lits0 + 4u ? 15u : litBump;  // a match was taken
+#pragma unroll
+          for (int r = 0; r < 4; r++) nwin = wrlane(nwin, mcost[r] << 6, 3u - (uint32_t)r);
+          win = nwin;
+        }
+        return 64u;
+      };
+      if (cmax <= 16u) tFast = fast(std::integral_constant<bool, true>());
+      else if (cmax <= 64u) tFast = fast(std::integral_constant<bool, false>());
+      if (tFast) chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
+    }
+    for (uint32_t t = tFast; t < 64; t += 4) {
       const int32_t i0 = hi - (int32_t)t;
       if (i0 < lo) break;
       // next batch's window, shifted by four lanes (lanes 0-3 are refilled below)
@@ -2926,6 +3291,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
 #pragma unroll
       for (int r = 0; r < 4; r++) nwin = wrlane(nwin, mcost[r] << 6, 3u - (uint32_t)r);
       win = nwin;
+    }
     }
     // flush: choices (a position took its best key iff its cost is that key's), costs to ring and HBM
     const int32_t iMine = hi - (int32_t)lane;
@@ -3727,12 +4093,17 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                          ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank,
                          (uint32_t)fuseSort);
-    else if (unlimited)
+    else if (unlimited) {
+      // big key groups first (left-maximal candidates + text-order prefix maximum), then pass 2
+      hipFuncSetAttribute((const void*)k_find_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
+      if (!getenv("SZ4_NO_BIG"))
+      hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
+                         compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
                            specDist, fix);
-    else
+    } else
       hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
                          compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
   } else {
@@ -3744,6 +4115,10 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {
+      hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+      if (!getenv("SZ4_NO_BIG"))
+      hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount, compact,
+                         scratch, longBits, segLong, mlen, mdist, matchBase, specLen);
       hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,

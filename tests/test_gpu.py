@@ -16,7 +16,10 @@ HDR = bytes([0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF])
 
 
 def expected_frame(data, bs, chain):
-    body = b"".join(pyoracle.oz_block(data[o:o + bs], chain) for o in range(0, len(data), bs))
+    # blocks are independent: the oracle runs them on threads (ctypes releases the GIL)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=8) as ex:
+        body = b"".join(ex.map(lambda o: pyoracle.oz_block(data[o:o + bs], chain), range(0, len(data), bs)))
     return HDR + body + b"\0\0\0\0"
 
 
@@ -82,6 +85,29 @@ def test_blocks_long_matches(compressor, name, data, bs, chains):
     repair pass across parse segments, the finder's early exit and pass-2 seed."""
     for chain in chains:
         assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain), chain
+
+
+SILESIA_KINDS = {
+    "db": synth._db_records, "xml": synth._xml_records, "exe": synth._opcodes,
+    "image": synth._image16, "src": synth._source,
+}
+
+
+@pytest.mark.parametrize("kind", sorted(SILESIA_KINDS))
+@pytest.mark.parametrize("bs", [65536, 262144])
+def test_blocks_structured_content(compressor, kind, bs):
+    """The Silesia-shaped generator's pieces on their own: fixed-width binary records (key groups of
+    tens of thousands of candidates: k_find_big's left-maximal search and text-order prefix maximum,
+    several segments per block at 256 KiB), XML records, an opcode stream, 16-bit images, source."""
+    data = SILESIA_KINDS[kind](600000 if bs > 65536 else 400000, np.random.default_rng(77))
+    for chain in (65535, 7) if kind != "db" else (65535,):
+        assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain), chain
+
+
+def test_blocks_silesia_mix_4m(compressor):
+    """configs[2]'s shape: Silesia-shaped mixed content in 4 MiB independent blocks."""
+    data = synth.silesia_like(5 << 20, seed=78)
+    assert compressor.compress_blocks(data, 4 << 20, 65535) == expected_frame(data, 4 << 20, 65535)
 
 
 def _skip_into_run(seed):
