@@ -374,21 +374,34 @@ def main():
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
         pmc_cfg = {"workload": args.workload, "bytes_per_gpu": nbytes, "block_size": bs, "level": args.level}
         pmc = pmc_traffic(pmc_cfg)
-        roof = {"kernel": "k_find_sorted (k_sort fused in)", "bound": "hbm", "achieved": round(achieved, 3),
+        # The kernel is bound by instruction issue (it checks every candidate of the reference's -9 hash
+        # chain), not by HBM: "bound" says so, achieved/peak/frac are its HBM
+        # roofline, "issue" its issue roofline from the SQ pass of the PMC profile
+        roof = {"kernel": "k_find_sorted (k_sort fused in)", "bound": "issue", "achieved": round(achieved, 3),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                 "traffic": pmc[1]["hbm_bytes_per_launch"] if pmc else None,
                 "algorithmic_bytes_per_launch": alg_bytes,
-                "limiter": "issue/latency: the kernel checks every candidate of the reference's -9 hash chain "
-                           "(DESIGN.md section 6); the HBM roofline fraction says how far it is from being "
-                           "memory bound",
+                "limiter": "instruction issue and latency (VALU candidate checks, SALU control): achieved/peak is "
+                           "the HBM roofline (algorithmic bytes per launch / launch time vs 8 TB/s), the issue "
+                           "roofline is under 'issue'",
                 "step_compulsory": {"bytes": nbytes + size, "GB/s": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world, 3),
                                     "frac": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world / HBM_PEAK_GBS, 6),
                                     "note": "input read + frame written per GPU per step over the whole step"}}
         if pmc:
             roof["traffic_source"] = os.path.relpath(pmc[0], ROOT)
-            for k in ("valu_per_simd_cycle", "salu_per_cu_cycle", "avg_duration_us"):
-                if k in pmc[1]:
-                    roof[k] = pmc[1][k]
+            rec_p = pmc[1]
+            if rec_p.get("hbm_bytes_per_launch"):
+                roof["traffic_over_algorithmic"] = round(rec_p["hbm_bytes_per_launch"] / alg_bytes, 3)
+            # issue roofline (MI355X_MICROARCH.md: a wave64 VALU instruction holds a SIMD-32 for 2 cycles
+            # -> 0.5 per SIMD-cycle; one scalar unit per CU -> 1 per CU-cycle)
+            issue = {"source": os.path.relpath(pmc[0], ROOT), "profiled_avg_duration_us": rec_p.get("avg_duration_us")}
+            if rec_p.get("valu_per_simd_cycle") is not None:
+                issue.update({"valu_per_simd_cycle": rec_p["valu_per_simd_cycle"], "valu_peak": 0.5,
+                              "valu_frac": round(rec_p["valu_per_simd_cycle"] / 0.5, 4)})
+            if rec_p.get("salu_per_cu_cycle") is not None:
+                issue.update({"salu_per_cu_cycle": rec_p["salu_per_cu_cycle"], "salu_peak": 1.0,
+                              "salu_frac": round(rec_p["salu_per_cu_cycle"], 4)})
+            roof["issue"] = issue
         rec = {
             "metric": METRIC,
             "value": round(value, 2),

@@ -1,0 +1,35 @@
+#!/usr/bin/env python3
+"""Diagnostic: k_find_sorted's per-wavefront counters from a SZ4_DIAG=3 build of the library
+(smallz4_amd/lib/libsmallz4_amd_diag.so, built by tools/build_diag.sh): below-chunk candidate steps
+(dB), shift-register steps (dL), improve calls (dBi), extension steps (dLi) and cycles per wave."""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["SMALLZ4_AMD_LIB"] = os.path.join(ROOT, "smallz4_amd", "lib", "libsmallz4_amd_diag.so")
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import smallz4_amd  # noqa: E402
+from smallz4_amd import synth  # noqa: E402
+
+mb = float(sys.argv[1]) if len(sys.argv) > 1 else 100
+chain = int(sys.argv[2]) if len(sys.argv) > 2 else 65535
+n = int(mb * 1e6)
+data = synth.enwik8_like(n, seed=8)
+comp = smallz4_amd.Compressor()
+comp.compress_blocks(data[:1 << 20], 65536, chain)
+comp.compress_blocks(data, 65536, chain)
+lib = comp._lib
+lib.sz4_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+nwaves = ((n + 65535) // 65536) * 16
+buf = np.zeros(nwaves * 8, dtype=np.uint64)
+assert lib.sz4_diag_read(buf.ctypes.data, buf.size) == 0
+d = buf.reshape(-1, 8).astype(np.float64)
+cyc = d[:, 1] - d[:, 0]
+print(f"waves {nwaves}: below-chunk steps dB {d[:, 2].sum():.4g}, shift steps dL {d[:, 3].sum():.4g}, "
+      f"improve dBi {d[:, 4].sum():.4g}, extension steps dLi {d[:, 5].sum():.4g}")
+print(f"per wave: dB {d[:, 2].mean():.1f} dL {d[:, 3].mean():.1f}; cycles mean {cyc.mean():.4g} max {cyc.max():.4g}")
+print(f"per position: dB {d[:, 2].sum() / n:.3f} dL {d[:, 3].sum() / n:.3f} (wave-steps per target position)")
