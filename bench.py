@@ -255,10 +255,18 @@ def main():
 
     import torch
     import torch.distributed as dist
+    # SZ4_BENCH_SHARE_DEVICE=1: every rank on GPU 0 with gloo collectives -- the sharded path rehearsed on
+    # a one-GPU box (tests/test_shards.py); RCCL does not take two ranks on one device
+    share = os.environ.get("SZ4_BENCH_SHARE_DEVICE") == "1"
+    if share:
+        local = 0
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     import smallz4_amd
@@ -333,7 +341,7 @@ def main():
 
     # whole-job results over ranks
     res = torch.tensor([elapsed, float(size), float(diff), float(verified), 0.0 if rt_ok else 1.0],
-                       dtype=torch.float64, device=dev)
+                       dtype=torch.float64, device="cpu" if share else dev)
     if world > 1:
         mx = res.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)

@@ -139,7 +139,7 @@ struct sz4_ctx {
   std::vector<Interval> ghostIv;
   bool ghost = false;
   uint32_t dictCont = 0, dictShift = 0, dictLow0 = 0;
-  DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut;  // decoder (sz4_unlz4*)
+  DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut, unSeq;  // decoder (sz4_unlz4*)
   std::vector<UnBlock> hUn;
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
@@ -170,7 +170,7 @@ struct sz4_ctx {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
             &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
-            &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut};
+            &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut, &unSeq};
   }
 
   int fail(int code, const char* what, hipError_t e = hipSuccess)
@@ -443,7 +443,9 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   const uint32_t nb = (uint32_t)meta[0];
   c->hUn.resize(nb);
   if (nb) {
-    launch_unlz4_sizes(f, n, c->unBlk.as<UnBlock>(), nb, s);
+    if ((e = c->unSeq.reserve(unlz4_seq_entries(n, nb) * sizeof(uint4) + 64)))
+      return c->fail(SZ4_E_NOMEM, "decoder sequences", e);
+    launch_unlz4_sizes(f, n, c->unBlk.as<UnBlock>(), nb, c->unSeq.as<uint4>(), s);
     if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
         (e = hipStreamSynchronize(s)))
       return c->fail(SZ4_E_DEVICE, "block sizes", e);
@@ -479,7 +481,7 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
   if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), keep * sizeof(UnBlock), hipMemcpyHostToDevice, s)) ||
       (e = hipMemsetAsync(flags, 0, flagBytes, s)))
     return c->fail(SZ4_E_DEVICE, "decoder plan", e);
-  launch_unlz4_blocks(f, n, c->unBlk.as<UnBlock>(), keep, out, dict, dl, flags, s);
+  launch_unlz4_blocks(f, n, c->unBlk.as<UnBlock>(), keep, c->unSeq.as<uint4>(), out, dict, dl, flags, s);
   if ((e = hipGetLastError()) || (e = hipMemcpyAsync(&status, flags + keep, 4, hipMemcpyDeviceToHost, s)) ||
       (e = hipStreamSynchronize(s)))
     return c->fail(SZ4_E_DEVICE, "decode", e);

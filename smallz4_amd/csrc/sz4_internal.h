@@ -140,11 +140,15 @@ struct UnBlock {
   uint64_t size;    // decoded bytes (k_unlz4_sizes), kNone when malformed
   uint32_t len;     // payload bytes
   uint32_t stored;  // 1: uncompressed block
+  uint32_t nseq;    // sequences recorded by k_unlz4_sizes
+  uint32_t pad;
 };
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s);
-void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, hipStream_t s);
+// sequence list: unlz4_seq_entries(frame length, blocks) uint4 entries (block bi's at src / 3 + 2 bi)
+uint64_t unlz4_seq_entries(uint64_t frameLen, uint32_t nb);
+void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, uint4* seq, hipStream_t s);
 // flags: nb done flags, then the status word, then the ticket (zeroed before the launch)
-void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, uint8_t* out, const uint8_t* dict,
-                         uint64_t dl, uint32_t* flags, hipStream_t s);
+void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, const uint4* seq, uint8_t* out,
+                         const uint8_t* dict, uint64_t dl, uint32_t* flags, hipStream_t s);
 
 }  // namespace sz4

@@ -6,17 +6,22 @@
 // than 8 MiB (smallz4cat.c:325-327).
 //
 //   k_unlz4_index   one lane walks the block size words (a dependent chain, smallz4cat.c:189-205)
-//   k_unlz4_sizes   one wavefront per block: token headers only -> decoded length, validation
+//   k_unlz4_sizes   one wavefront per block: token headers only -> decoded length, validation, and
+//                   the block's sequence list (literal run, match length, offset, frame offset of
+//                   the literals), recorded 64 at a time as coalesced 16-byte entries
 //   (host)          output offset of every block, legacy truncation, capacity check
-//   k_unlz4_blocks  one wavefront per block: token headers from a 256-byte register window, literal
-//                   and match bytes 64 per step, the block's last 64 KiB of output in an LDS ring
-//                   (the reference's history[], smallz4cat.c:161-166).  A match reaching below the
-//                   block start waits for the blocks it reads: blocks are claimed in order through
-//                   a ticket (placement independent), each publishes a done flag (agent release),
-//                   a waiter polls relaxed, then acquires; every spin is bounded.
+//   k_unlz4_blocks  one wavefront per block replays its sequence list, 64 sequences per step: their
+//                   output offsets by one wavefront scan, their literal bytes prefetched into
+//                   registers (a 512-byte frame window) and picked with ds_bpermute, then per
+//                   sequence the literals and the match 64 bytes per step through the block's last
+//                   64 KiB of output in an LDS ring (the reference's history[], smallz4cat.c:161-166).
+//                   No header parsing and no global load on the sequence chain.  A match reaching
+//                   below the block start waits for the blocks it reads: blocks are claimed in order
+//                   through a ticket (placement independent), each publishes a done flag (agent
+//                   release), a waiter polls relaxed, then acquires; every spin is bounded.
 //
-// Byte work only: decoding one block is a chain of token headers, so the parallelism is one
-// wavefront per block and 64 bytes per copy step.
+// Byte work only: decoding one block is a chain of sequences (each match may read the bytes the one
+// before it wrote), so the parallelism is one wavefront per block and 64 bytes per copy step.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -57,28 +62,58 @@ struct Window {
 
 constexpr uint64_t kWaitLimit = 100000000ull * 60;  // 60 s of s_memrealtime (100 MHz)
 
-// Decode (kWrite) or measure (!kWrite) one block.  Returns its decoded length, or kNone when it is
-// malformed the way oz_unlz4 rejects it: a length byte, literal run or offset running past the
-// block, or offset 0 (smallz4cat.c:212-323).
-template <bool kWrite>
-__device__ uint64_t unlz4_block(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t bi, uint32_t lane,
-                                uint8_t* __restrict__ out, uint8_t* __restrict__ ring, const uint8_t* __restrict__ dict,
-                                uint64_t dl, const UnBlock* __restrict__ blk, uint32_t* __restrict__ done,
-                                uint32_t* __restrict__ status)
+// v_writelane (the LLVM intrinsic by name): lane `l` of v becomes the uniform `x`
+extern "C" __device__ int sz4_un_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ uint32_t un_wrlane(uint32_t v, uint32_t x, uint32_t l)
 {
-  if (B.stored) {
-    // uncompressed block (smallz4cat.c:329-343): later blocks read it from `out`
-    if (kWrite)
-      for (uint64_t k = lane; k < B.len; k += 64) out[B.dst + k] = f[B.src + k];
-    return B.len;
+  return (uint32_t)sz4_un_writelane((int)x, (int)l, (int)v);
+}
+
+__device__ __forceinline__ uint32_t un_incl_scan_add(uint32_t v, uint32_t lane)
+{
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += o;
   }
+  return v;
+}
+
+// Sequence list of block bi: at most len/3 + 2 entries (a sequence with a match takes >= 3 frame
+// bytes), at seqAll + src/3 + 2 * bi -- disjoint from every other block's, no host prefix needed.
+__device__ __forceinline__ uint4* seq_base(uint4* seqAll, const UnBlock& B, uint32_t bi)
+{
+  return seqAll + B.src / 3 + 2ull * bi;
+}
+__device__ __forceinline__ uint32_t seq_cap(const UnBlock& B) { return B.len / 3 + 2; }
+
+// Header walk of one block (smallz4cat.c:212-323): its decoded length, or kNone when it is malformed
+// the way oz_unlz4 rejects it (a length byte, literal run or offset running past the block, offset 0).
+// Every sequence is recorded as (literals, match length, offset, frame offset of the literals from
+// B.src): lane l holds entry (count & ~63) + l until 64 are complete, then one coalesced store.
+__device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane,
+                                uint4* __restrict__ seq, uint32_t* nseq)
+{
+  *nseq = 0;
+  if (B.stored) return B.len;  // uncompressed block (smallz4cat.c:329-343)
   const uint64_t end = B.src + B.len;
-  uint64_t r = B.src, w = 0;  // frame cursor; bytes decoded so far (output position B.dst + w)
-  uint64_t floorPos = B.dst;  // output below this is read only after its blocks are done
-  uint32_t waitIdx = bi;
+  const uint32_t cap = seq_cap(B);
+  uint64_t r = B.src, w = 0;  // frame cursor; bytes decoded so far
+  uint32_t ns = 0;
+  uint4 buf = make_uint4(0u, 0u, 0u, 0u);
+  auto push = [&](uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel) {
+    const uint32_t l = ns & 63u;
+    buf.x = un_wrlane(buf.x, lits, l);
+    buf.y = un_wrlane(buf.y, ml, l);
+    buf.z = un_wrlane(buf.z, off, l);
+    buf.w = un_wrlane(buf.w, frel, l);
+    ns++;
+    if ((ns & 63u) == 0u) seq[ns - 64u + lane] = buf;
+  };
   Window win{f, n, 0, 0};
   win.fill(r, lane);
   while (r < end) {
+    if (ns >= cap) return kNone;  // cannot happen in a well-formed block
     const uint32_t tok = win.byte(r++, lane);
     uint64_t lits = tok >> 4;
     if (lits == 15) {
@@ -90,29 +125,13 @@ __device__ uint64_t unlz4_block(const uint8_t* __restrict__ f, uint64_t n, const
       } while (x == 255);
     }
     if (r + lits > end) return kNone;
-    if (kWrite && lits) {
-      const uint64_t P = B.dst + w;
-      if (lits <= 64) {
-        // lane j takes byte r + j out of the register window
-        if (r + lits > win.base + 256) win.fill(r, lane);
-        const uint32_t rel = (uint32_t)(r - win.base) + lane;
-        const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((rel >> 2) << 2), (int)win.w);
-        const uint8_t v = (uint8_t)(word >> (8 * (rel & 3)));
-        if (lane < lits) {
-          out[P + lane] = v;
-          ring[(P + lane) & 0xFFFFu] = v;
-        }
-      } else {
-        for (uint64_t k = lane; k < lits; k += 64) {
-          const uint8_t v = f[r + k];
-          out[P + k] = v;
-          ring[(P + k) & 0xFFFFu] = v;
-        }
-      }
-    }
+    const uint32_t frel = (uint32_t)(r - B.src);
     w += lits;
     r += lits;
-    if (r == end) break;  // the last sequence has literals only
+    if (r == end) {  // the last sequence has literals only
+      push((uint32_t)lits, 0u, 0u, frel);
+      break;
+    }
     if (r + 2 > end) return kNone;
     const uint32_t off = win.byte(r, lane) | (win.byte(r + 1, lane) << 8);
     r += 2;
@@ -126,50 +145,127 @@ __device__ uint64_t unlz4_block(const uint8_t* __restrict__ f, uint64_t n, const
         ml += x;
       } while (x == 255);
     }
-    if (kWrite) {
-      const uint64_t P = B.dst + w;
-      const int64_t lo = (int64_t)P - (int64_t)off;  // lowest byte this match reads
-      if (lo < (int64_t)floorPos && floorPos > 0 && waitIdx > 0) {
-        // the blocks holding output in [max(lo, 0), floorPos) must be finished
-        while (waitIdx > 0 && (int64_t)floorPos > lo && floorPos > 0) {
-          waitIdx--;
-          if (lane == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            while (__hip_atomic_load(&done[waitIdx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-              __builtin_amdgcn_s_sleep(8);
-              if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitLimit) {
-                atomicOr(status, 2u);  // give up: the result is flagged, the grid still drains
-                break;
-              }
-            }
-          }
-          floorPos = blk[waitIdx].dst;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      // output P + j = output P + j - off.  First step: lane j reads P - off + (j mod off), all
-      // written before the match.  Later steps read P + j - q with q the smallest multiple of off
-      // that is >= 64: the previous step's bytes (period off), so the ring never needs more than
-      // 64 KiB even for matches longer than that.
-      const uint32_t q = off >= 64u ? off : off * ((64u + off - 1u) / off);
-      for (uint64_t k = 0; k < ml; k += 64) {
-        const uint64_t j = k + lane;
-        const int64_t s = k == 0 ? lo + (int64_t)(off >= 64u ? lane : lane % off) : (int64_t)(P + j) - (int64_t)q;
-        uint8_t v = 0;
-        if (j < ml) {
-          if (s >= (int64_t)B.dst) v = ring[(uint64_t)s & 0xFFFFu];
-          else if (s >= 0) v = out[s];                                   // an earlier block (finished)
-          else if ((uint64_t)(-s) <= dl) v = dict[dl - (uint64_t)(-s)];  // the dictionary's tail
-          // else 0: before the history (oz_unlz4's zero-initialised history)
-        }
-        if (j < ml) {
-          out[P + j] = v;
-          ring[(P + j) & 0xFFFFu] = v;
+    push((uint32_t)lits, (uint32_t)ml, off, frel);
+    w += ml;
+  }
+  if (ns & 63u) {
+    const uint32_t b = ns & ~63u;
+    if (lane < (ns & 63u)) seq[b + lane] = buf;
+  }
+  *nseq = ns;
+  return w;
+}
+
+// Replays block bi's sequence list into `out` (and the ring); returns the decoded length.
+__device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t bi, uint32_t lane,
+                                 const uint4* __restrict__ seq, uint8_t* __restrict__ out, uint8_t* __restrict__ ring,
+                                 const uint8_t* __restrict__ dict, uint64_t dl, const UnBlock* __restrict__ blk,
+                                 uint32_t* __restrict__ done, uint32_t* __restrict__ status)
+{
+  if (B.stored) {
+    // later blocks read it from `out`
+    for (uint64_t k = lane; k < B.len; k += 64) out[B.dst + k] = f[B.src + k];
+    return B.len;
+  }
+  uint64_t floorPos = B.dst;  // output below this is read only after its blocks are done
+  uint32_t waitIdx = bi;
+  uint64_t w = 0;             // bytes decoded so far
+  for (uint32_t b0 = 0; b0 < B.nseq; b0 += 64) {
+    const uint32_t cnt = B.nseq - b0 < 64u ? B.nseq - b0 : 64u;
+    const uint4 q = lane < cnt ? seq[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+    // output offset of every sequence's literals (a wavefront scan of literals + match length)
+    const uint32_t tot = q.x + q.y;
+    const uint32_t incl = un_incl_scan_add(tot, lane);
+    const uint64_t pos = w + (incl - tot);
+    // the frame bytes of the 64 sequences' literals in registers when they span <= 512 bytes: lane l
+    // holds [fb + 8l, fb + 8l + 8)
+    const uint64_t fb = (B.src + un_rdlane(q.w, 0)) & ~7ull;
+    const uint64_t fe = B.src + un_rdlane(q.w + q.x, cnt - 1u);
+    const bool inWin = fe - fb <= 512u;
+    uint32_t w0 = 0, w1 = 0;
+    if (inWin) {
+      const uint64_t o = fb + 8ull * lane;
+      if (o + 8 <= n && (reinterpret_cast<uintptr_t>(f) & 7u) == 0u) {
+        const uint2 v = *reinterpret_cast<const uint2*>(f + o);
+        w0 = v.x;
+        w1 = v.y;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+          const uint32_t b = o + k < n ? (uint32_t)f[o + k] : 0u;
+          if (k < 4) w0 |= b << (8 * k);
+          else w1 |= b << (8 * (k - 4));
         }
       }
     }
-    w += ml;
+    for (uint32_t j = 0; j < cnt; j++) {
+      const uint32_t L = un_rdlane(q.x, j), M = un_rdlane(q.y, j), off = un_rdlane(q.z, j), fr = un_rdlane(q.w, j);
+      const uint64_t P = B.dst + (uint64_t)un_rdlane((uint32_t)pos, j);  // a block decodes to < 2^32 bytes
+      if (L) {
+        if (inWin && L <= 64u) {
+          // lane k takes byte k out of the register window
+          const uint32_t rel = (uint32_t)(B.src + fr - fb) + lane;
+          const int addr = (int)((rel >> 3) << 2);
+          const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)w0);
+          const uint32_t c = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)w1);
+          const uint8_t v = (uint8_t)(((rel & 4u) ? c : a) >> (8 * (rel & 3u)));
+          if (lane < L) {
+            out[P + lane] = v;
+            ring[(P + lane) & 0xFFFFu] = v;
+          }
+        } else {
+          for (uint64_t k = lane; k < L; k += 64) {
+            const uint8_t v = f[B.src + fr + k];
+            out[P + k] = v;
+            ring[(P + k) & 0xFFFFu] = v;
+          }
+        }
+      }
+      if (M) {
+        const uint64_t Q = P + L;                     // the match's first output byte
+        const int64_t lo = (int64_t)Q - (int64_t)off;  // lowest byte it reads
+        if (lo < (int64_t)floorPos && floorPos > 0 && waitIdx > 0) {
+          // the blocks holding output in [max(lo, 0), floorPos) must be finished
+          while (waitIdx > 0 && (int64_t)floorPos > lo && floorPos > 0) {
+            waitIdx--;
+            if (lane == 0) {
+              const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+              while (__hip_atomic_load(&done[waitIdx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+                __builtin_amdgcn_s_sleep(8);
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kWaitLimit) {
+                  atomicOr(status, 2u);  // give up: the result is flagged, the grid still drains
+                  break;
+                }
+              }
+            }
+            floorPos = blk[waitIdx].dst;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // output Q + j = output Q + j - off.  First step: lane j reads Q - off + (j mod off), all
+        // written before the match.  Later steps read Q + j - q with q the smallest multiple of off
+        // that is >= 64: the previous step's bytes (period off), so the ring never needs more than
+        // 64 KiB even for matches longer than that.
+        const uint32_t qq = off >= 64u ? off : off * ((64u + off - 1u) / off);
+        for (uint64_t k = 0; k < M; k += 64) {
+          const uint64_t jj = k + lane;
+          const int64_t s = k == 0 ? lo + (int64_t)(off >= 64u ? lane : lane % off) : (int64_t)(Q + jj) - (int64_t)qq;
+          uint8_t v = 0;
+          if (jj < M) {
+            if (s >= (int64_t)B.dst) v = ring[(uint64_t)s & 0xFFFFu];
+            else if (s >= 0) v = out[s];                                   // an earlier block (finished)
+            else if ((uint64_t)(-s) <= dl) v = dict[dl - (uint64_t)(-s)];  // the dictionary's tail
+            // else 0: before the history (oz_unlz4's zero-initialised history)
+          }
+          if (jj < M) {
+            out[Q + jj] = v;
+            ring[(Q + jj) & 0xFFFFu] = v;
+          }
+        }
+      }
+    }
+    w += un_rdlane(incl, cnt - 1u);
   }
   return w;
 }
@@ -239,19 +335,23 @@ __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ 
 }
 
 __global__ __launch_bounds__(64) void k_unlz4_sizes(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
-                                                    uint32_t nb)
+                                                    uint32_t nb, uint4* __restrict__ seqAll)
 {
   const uint32_t bi = blockIdx.x, lane = threadIdx.x;
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
-  const uint64_t size = unlz4_block<false>(f, n, B, bi, lane, nullptr, nullptr, nullptr, 0, nullptr, nullptr, nullptr);
-  if (lane == 0) blk[bi].size = size;
+  uint32_t ns = 0;
+  const uint64_t size = unlz4_parse(f, n, B, lane, seq_base(seqAll, B, bi), &ns);
+  if (lane == 0) {
+    blk[bi].size = size;
+    blk[bi].nseq = ns;
+  }
 }
 
 // flags[0..nb) done flags, flags[nb] status bits, flags[nb + 1] ticket (all zeroed before the launch)
 __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
-                                                     uint32_t nb, uint8_t* __restrict__ out, const uint8_t* __restrict__ dict,
-                                                     uint64_t dl, uint32_t* __restrict__ flags)
+                                                     uint32_t nb, const uint4* __restrict__ seqAll, uint8_t* __restrict__ out,
+                                                     const uint8_t* __restrict__ dict, uint64_t dl, uint32_t* __restrict__ flags)
 {
   __shared__ uint8_t ring[65536];
   const uint32_t lane = threadIdx.x;
@@ -264,7 +364,8 @@ __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__
   const uint32_t bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
-  const uint64_t got = unlz4_block<true>(f, n, B, bi, lane, out, ring, dict, dl, blk, done, status);
+  const uint64_t got = unlz4_decode(f, n, B, bi, lane, seq_base(const_cast<uint4*>(seqAll), B, bi), out, ring, dict, dl, blk,
+                                    done, status);
   if (lane == 0 && got != B.size) atomicOr(status, 1u);
   // publish: this wave's stores drained, written back (agent release), then the flag
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -278,15 +379,17 @@ void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t max
   hipLaunchKernelGGL(k_unlz4_index, dim3(1), dim3(64), 0, s, f, n, blk, maxBlocks, meta);
 }
 
-void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, hipStream_t s)
+uint64_t unlz4_seq_entries(uint64_t frameLen, uint32_t nb) { return frameLen / 3 + 2ull * nb + 2; }
+
+void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, uint4* seq, hipStream_t s)
 {
-  if (nb) hipLaunchKernelGGL(k_unlz4_sizes, dim3(nb), dim3(64), 0, s, f, n, blk, nb);
+  if (nb) hipLaunchKernelGGL(k_unlz4_sizes, dim3(nb), dim3(64), 0, s, f, n, blk, nb, seq);
 }
 
-void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, uint8_t* out, const uint8_t* dict,
-                         uint64_t dl, uint32_t* flags, hipStream_t s)
+void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, const uint4* seq, uint8_t* out,
+                         const uint8_t* dict, uint64_t dl, uint32_t* flags, hipStream_t s)
 {
-  if (nb) hipLaunchKernelGGL(k_unlz4_blocks, dim3(nb), dim3(64), 0, s, f, n, blk, nb, out, dict, dl, flags);
+  if (nb) hipLaunchKernelGGL(k_unlz4_blocks, dim3(nb), dim3(64), 0, s, f, n, blk, nb, seq, out, dict, dl, flags);
 }
 
 }  // namespace sz4

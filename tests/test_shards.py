@@ -79,3 +79,25 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
     assert footprint < 120 * len(data) + (1 << 30)
+
+
+@pytest.mark.parametrize("workload,mb,sample", [("enwik9", 8, 16), ("zeros_urandom", 4, 2)])
+def test_bench_two_ranks_shard_one_input(workload, mb, sample):
+    """`bench.py --gpus 2` end to end on the one-GPU box: two processes (a torch.distributed.run child
+    started by bench.py itself), each compressing its block range of ONE input through the HIP
+    library; both ranks on GPU 0 with gloo collectives (SZ4_BENCH_SHARE_DEVICE=1; the 8-GPU run uses
+    RCCL, one device per rank).  The line must report 2 ranks, the whole input, a zero byte diff on
+    every rank's sample and both device round trips."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SZ4_BENCH_SHARE_DEVICE="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", workload,
+                        "--mb", str(mb), "--steps", "2", "--warmup", "1", "--verify-blocks", str(sample),
+                        "--no-stream"], capture_output=True, text=True, timeout=400, cwd=root, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert rec["n_gpus"] == 2 and rec["config"]["input_bytes"] == 2 * mb * 1_000_000, rec
+    assert rec["byte_diff"] == 0 and rec["blocks_verified"] >= 2 * sample and rec["roundtrip_ok"], rec
