@@ -705,6 +705,9 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
   // exact key of each lane among them
   __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
   __shared__ uint32_t s_satBest[kFindThreads / 64][64];
+#if SZ4_DIAG == 3
+  const uint64_t tEntry = __builtin_readcyclecounter();
+#endif
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1074,6 +1077,9 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
     }
     if (unlimited && __ballot(active && isLong) && lane == 0) s_long = 1;
   }
+#if SZ4_DIAG == 3
+  const uint64_t tSearch = __builtin_readcyclecounter();
+#endif
   __syncthreads();
   if (tid == 0) segLong[blockIdx.x] = s_long;
 
@@ -1121,7 +1127,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
   const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
   if (lane == 0 && w * 8 + 8 <= (1u << 20)) {
     uint64_t* d = sz4_diag + w * 8;
-    d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = 0; d[7] = 0;
+    d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = tEntry; d[7] = tSearch;
   }
 #endif
 }
@@ -1829,7 +1835,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
                                                            const uint2* __restrict__ compactAll, uint2* __restrict__ scratchAll,
                                                            uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
                                                            uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                           uint64_t matchBase, uint32_t* __restrict__ lm)
+                                                           uint64_t matchBase, uint32_t* __restrict__ lm, uint64_t* __restrict__ segTail,
+                                                           uint32_t resolveOnly)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_groups[2 * kMaxBigGroups];
@@ -1865,7 +1872,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   __syncthreads();
   const uint32_t ng = s_ng;
   if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
+  const uint64_t stopAbs = B.end - kTailLiterals;
 
+  // the second launch only resolves: a segment's first big targets need its predecessor segment's
+  // last results, final after the first launch
+  if (!resolveOnly) {
   typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
   {
     const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
@@ -1878,7 +1889,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       src.in = in;
     }
   }
-  const uint64_t stopAbs = B.end - kTailLiterals;
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
   auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
@@ -2005,6 +2015,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     }
     __syncthreads();
   }
+  }
   __threadfence_block();
   __syncthreads();
 
@@ -2062,8 +2073,16 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     bool cValid = false;
     uint64_t cKey = 0;
     if (phase == 1) {
-      // carry-in: the block's first target has no predecessor (exact state, nothing to carry)
+      // carry-in: the block's first target has no predecessor (exact state, nothing to carry); a later
+      // segment's first target takes its predecessor's result once that is final (not marked)
       cValid = S.s0 == B.start;
+      if (!cValid && resolveOnly && blockIdx.x > 0 && segs[blockIdx.x - 1].block == S.block) {
+        // the resolve launch: the state after the predecessor segment's last target, as the first
+        // launch left it (final then: no launch writes it afterwards)
+        const uint64_t t = segTail[blockIdx.x - 1];
+        cValid = (t >> 63) != 0u;
+        cKey = t & ~(1ull << 63);
+      }
       for (uint32_t w = 0; w < wave; w++) {
         if (s_hasHead[w]) {
           cValid = s_outValid[w] != 0u;
@@ -2105,6 +2124,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       s_hasHead[wave] = anyHead ? 1u : 0u;
       s_outValid[wave] = cValid ? 1u : 0u;
       s_outKey[wave] = cKey;
+    }
+    if (phase == 1 && !resolveOnly && lane == 0 && r1 == nTg && r0 < r1) {
+      // the state after the segment's last target, as a carry into the next segment (its s0 is our s1):
+      // ends E = i + len are relative to our s0, so the next segment's are E - nTg
+      const uint64_t e = cKey >> 16;
+      const uint64_t k = e > (uint64_t)nTg + kMinMatch - 1u ? ((e - nTg) << 16) | (cKey & 0xFFFFu) : 0ull;
+      segTail[blockIdx.x] = cValid ? (1ull << 63) | k : 0ull;
     }
     __syncthreads();
   }
@@ -2747,23 +2773,6 @@ __device__ __forceinline__ bool lazy_fast_block(const uint32_t* ivCount, const u
   return ivCount[b] == 0u && (longFlag[b] & kFlagRun) == 0u;
 }
 
-// index of the k-th set bit of m (0-based; k < popcount(m)), uniform
-__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t k)
-{
-  uint32_t base = 0;
-#pragma unroll
-  for (uint32_t w = 32; w >= 1; w >>= 1) {
-    const uint64_t lowMask = (w == 64) ? ~0ull : ((1ull << w) - 1ull);
-    const uint32_t c = (uint32_t)__popcll(m & lowMask);
-    if (k >= c) {
-      k -= c;
-      m >>= w;
-      base += w;
-    }
-  }
-  return base;
-}
-
 // the searched-position chain over a register window of lengths: four 64-position windows in
 // registers, loads three windows ahead (as k_walk); wave-uniform state
 struct LazyWalker {
@@ -2800,7 +2809,12 @@ struct LazyWalker {
       }
       const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch) & (~0ull << (pos - wbase));
       const uint32_t pc = (uint32_t)__popcll(mask);
-      if (need < pc) return wbase + select64(mask, need);
+      if (need < pc) {
+        // the set bit with exactly `need` set bits below it: each lane counts its own (mbcnt)
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        const uint64_t hit = __ballot(((mask >> lane_id()) & 1ull) && below == need);
+        return wbase + (uint32_t)__builtin_ctzll(hit);
+      }
       need -= pc;
       pos = wbase + 64;
     }
@@ -4076,8 +4090,8 @@ uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
                  const uint32_t* ivCount, uint2* compact, uint2* scratch, uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* longBits, uint32_t* segLong,
-                 uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist, bool ldsWindow, uint32_t hybridLds,
-                 bool fuseSort, hipStream_t s)
+                 uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist, uint64_t* segTail, bool ldsWindow,
+                 uint32_t hybridLds, bool fuseSort, hipStream_t s)
 {
   static_assert(sizeof(SortLds) <= 65536, "the fused sort's shared memory must fit the window buffer");
   static_assert(kOutTile * 4u <= 65536u + 16u, "a result tile must fit the window buffer");
@@ -4097,8 +4111,9 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       // big key groups first (left-maximal candidates + text-order prefix maximum), then pass 2
       hipFuncSetAttribute((const void*)k_find_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       if (!getenv("SZ4_NO_BIG"))
-      hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
-                         compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen);
+        for (uint32_t resolve = 0; resolve < 2; resolve++)
+          hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
@@ -4117,8 +4132,9 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     else if (unlimited) {
       hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       if (!getenv("SZ4_NO_BIG"))
-      hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount, compact,
-                         scratch, longBits, segLong, mlen, mdist, matchBase, specLen);
+        for (uint32_t resolve = 0; resolve < 2; resolve++)
+          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount,
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
       hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
