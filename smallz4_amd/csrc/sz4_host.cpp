@@ -128,7 +128,7 @@ struct sz4_ctx {
   bool separateSort = false;  // k_sort runs inside k_find_sorted; SZ4_SEPARATE_SORT=1: its own launch
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
-  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong;
+  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf chunkOut;             // stream path: one chunk's blocks
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
@@ -169,7 +169,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
             &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut, &unSeq};
   }
 
@@ -283,6 +283,7 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->longFlag.reserve(nb * 4 + 64)) ||
       (e = c->longBits.reserve(stagedBytes / 8 + 64)) ||
       (e = c->segLong.reserve(c->hSegs.size() * 4 + 64)) ||
+      (e = c->segTail.reserve(c->hSegs.size() * 8 + 64)) ||
       (e = c->rmqUp.reserve((stagedBytes + nb + 8) * 4)) ||
       (e = c->rmqDown.reserve((stagedBytes + nb + 8) * 4)))
     return c->fail(SZ4_E_NOMEM, "device allocation", e);
@@ -358,14 +359,14 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
     if (maxChain > 0)
       launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                  nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, !c->separateSort, s);
+                  nullptr, nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, !c->separateSort, s);
     mark(c, 3, s);
     if (c->stopAfter == 2) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     if (maxChain > 0)
       launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                  c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->ldsWindow, c->hybridLds,
-                  false, s);
+                  c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->segTail.as<uint64_t>(),
+                  c->ldsWindow, c->hybridLds, false, s);
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel.as<uint32_t>(),

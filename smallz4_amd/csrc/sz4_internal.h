@@ -99,12 +99,13 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
 // k_sort's work for its segment first (compact = sorted slot arrays, scratch = sort buffer, rank written)
 // scratch: per-slot words free after k_sort (the skip pointers of k_find_long9); longBits: one bit per
 // position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target;
-// specLen/specDist: per position words free before the parse (speculative carries of pass-2 piece heads)
+// specLen/specDist: per position words free before the parse (k_find_big's left-maximal results, then the
+// speculative carries of pass-2 piece heads); segTail: per segment, k_find_big's state after its last target
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
                  const Interval* iv, const uint32_t* ivCount, uint2* compact, uint2* scratch,
                  uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
-                 bool ldsWindow, uint32_t hybridLds, bool fuseSort, hipStream_t s);
+                 uint64_t* segTail, bool ldsWindow, uint32_t hybridLds, bool fuseSort, hipStream_t s);
 // dictionary mode: one wavefront replays the reference's match loop (dictBack = first insertion offset
 // before the first block); last: 2^20 u32, prevH / prevX: 65536 u16 each -- the reference's tables,
 // kept in HBM between the chunks of one stream.  cont: the first block continues the stream of the

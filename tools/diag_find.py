@@ -21,7 +21,9 @@ n = int(mb * 1e6)
 data = synth.enwik8_like(n, seed=8)
 comp = smallz4_amd.Compressor()
 comp.compress_blocks(data[:1 << 20], 65536, chain)
+comp.set_timing(True)
 comp.compress_blocks(data, 65536, chain)
+find_ms = comp.last_stage_ms()['find_sorted']
 lib = comp._lib
 lib.sz4_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 nwaves = ((n + 65535) // 65536) * 16
@@ -32,4 +34,10 @@ cyc = d[:, 1] - d[:, 0]
 print(f"waves {nwaves}: below-chunk steps dB {d[:, 2].sum():.4g}, shift steps dL {d[:, 3].sum():.4g}, "
       f"improve dBi {d[:, 4].sum():.4g}, extension steps dLi {d[:, 5].sum():.4g}")
 print(f"per wave: dB {d[:, 2].mean():.1f} dL {d[:, 3].mean():.1f}; cycles mean {cyc.mean():.4g} max {cyc.max():.4g}")
+t_entry, t_search = d[:, 6], d[:, 7]
+ok = t_entry > 0
+span = d[ok, 1].max() - t_entry[ok].min()
+print(f"phases per wave (ticks): sort {(d[ok, 0] - t_entry[ok]).mean():.4g}, "
+      f"window load + search {(t_search[ok] - d[ok, 0]).mean():.4g}, text-order output {(d[ok, 1] - t_search[ok]).mean():.4g}; "
+      f"kernel span {span:.4g} ticks in {find_ms:.3f} ms -> {span / find_ms / 1e6:.3f} GHz")
 print(f"per position: dB {d[:, 2].sum() / n:.3f} dL {d[:, 3].sum() / n:.3f} (wave-steps per target position)")
