@@ -29,6 +29,9 @@
 #ifndef SZ4_SPEC_ATTR
 #define SZ4_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))  // 8 waves/SIMD (SGPR spills to lanes are cheap)
 #endif
+#ifndef SZ4_LEAN_SHIFT
+#define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
+#endif
 #ifndef SZ4_DIAG
 #define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
 #endif
@@ -914,6 +917,27 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         }
       };
       // 1. inside the chunk: shift register (after s shifts lane l holds slot first + l - s)
+#if SZ4_LEAN_SHIFT
+      if (!needWin) {
+        // no window test: lane l has slot - max(gs, first) candidates inside the chunk, so the walk is
+        // a uniform trip count (the longest of them) with a per-lane bound -- no per-step walk flags
+        const int32_t lo1 = (int32_t)(gs > first ? gs : first);
+        const uint32_t myCnt = run && (int32_t)slot > lo1 ? (uint32_t)((int32_t)slot - lo1) : 0u;
+        const uint32_t rm = row_max(myCnt);
+        const uint32_t trips = max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
+        uint32_t r0 = me0, r1 = me1, r2 = me2;
+        for (uint32_t s = 1; s <= trips; s++) {
+#if SZ4_DIAG == 3
+          dL++;
+#endif
+          r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
+          r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
+          r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
+          visit(s <= myCnt, slot - s, r0, r1, r2);
+        }
+        run = run && (int32_t)gs < (int32_t)first;
+      } else
+#endif
       {
         const int32_t lo1 = (int32_t)(gs > first ? gs : first);
         uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
