@@ -29,6 +29,9 @@
 #ifndef SZ4_SPEC_ATTR
 #define SZ4_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))  // 8 waves/SIMD (SGPR spills to lanes are cheap)
 #endif
+#ifndef SZ4_SHIFT_UNROLL
+#define SZ4_SHIFT_UNROLL 1
+#endif
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
@@ -898,6 +901,26 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       };
       // lanes whose match can still grow past 12 bytes
       const uint64_t satOk = __ballot(limit > 12u);
+      // the same for a candidate every lane takes: its key, and x0 | x1 | x2 (0: all 12 bytes equal)
+      auto score = [&](uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
+        const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);  // ~0u when zero
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        const uint32_t lcp = min(4u + (z >> 3), cap12);
+        const uint32_t key = x0 == 0u ? (lcp << 17) | cs : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+        return x0 | x1 | x2;
+      };
+      // queue the lanes of `sat` (12 bytes equal, may grow past them) with candidate slot cs
+      auto enqueue = [&](uint64_t sat, uint32_t cs) {
+        if (sat) {
+          const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
+          if ((sat >> lane) & 1ull) satQ[at] = (lane << 17) | cs;
+          qn += (uint32_t)__builtin_popcountll(sat);
+          if (qn >= 64) flush();
+        }
+      };
       // one candidate for this lane: slot cs with first 12 bytes k0..k2.  The common prefix is
       // 4 + (trailing zero bits of x2:x1) / 8; a candidate from another hash group never has x0 = 0
       auto visit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
@@ -926,7 +949,30 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         const uint32_t rm = row_max(myCnt);
         const uint32_t trips = max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
         uint32_t r0 = me0, r1 = me1, r2 = me2;
-        for (uint32_t s = 1; s <= trips; s++) {
+        uint32_t s = 1;
+#if SZ4_SHIFT_UNROLL
+        // two shifts per step, one saturation test for the two (four would exceed 64 VGPRs: 8 waves/SIMD)
+        for (; s + 1 <= trips; s += 2) {
+#if SZ4_DIAG == 3
+          dL += 2;
+#endif
+          uint32_t xs[2];
+#pragma unroll
+          for (uint32_t u = 0; u < 2; u++) {
+            r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
+            r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
+            r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
+            const bool mine = s + u <= myCnt;
+            const uint32_t x = score(mine ? slot - s - u : 0u, mine ? r0 : ~me0, r1, r2);
+            xs[u] = mine ? x : 0xFFFFFFFFu;
+          }
+          if (__ballot(min(xs[0], xs[1]) == 0u) & satOk) {
+#pragma unroll
+            for (uint32_t u = 0; u < 2; u++) enqueue(__ballot(xs[u] == 0u) & satOk, slot - s - u);
+          }
+        }
+#endif
+        for (; s <= trips; s++) {
 #if SZ4_DIAG == 3
           dL++;
 #endif
