@@ -1026,7 +1026,19 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
           } else {
             // no window test: every lane may take the candidate (only the group's lanes can match; a
             // lane finished at its cap cannot move: its queued candidates never beat the one it has)
-            for (int32_t k = 0; k < n; k++) {
+            int32_t k = 0;
+            for (; k + 1 < n; k += 2) {
+#if SZ4_DIAG == 3
+              dB += 2;
+#endif
+              const uint32_t xa = score((uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              const uint32_t xb = score((uint32_t)(cBase - k - 1), rdlane(f0, k + 1), rdlane(f1, k + 1), rdlane(f2, k + 1));
+              if (__ballot(min(xa, xb) == 0u) & satOk) {
+                enqueue(__ballot(xa == 0u) & satOk, (uint32_t)(cBase - k));
+                enqueue(__ballot(xb == 0u) & satOk, (uint32_t)(cBase - k - 1));
+              }
+            }
+            for (; k < n; k++) {
 #if SZ4_DIAG == 3
               dB++;
 #endif
