@@ -1018,6 +1018,14 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
           const uint64_t fp = S.w0 + fRel;
           const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
+#if SZ4_DIAG == 3
+          {
+            // broadcast steps that serve at most 32 / at most 8 of the chunk's lanes
+            const uint32_t nr = (uint32_t)__builtin_popcountll(__ballot(run));
+            if (nr <= 32u) dBi += (uint64_t)n;
+            if (nr <= 8u) dLi += (uint64_t)n;
+          }
+#endif
           if (needWin) {
             for (int32_t k = 0; k < n; k++) {
               if (run && rdlane(fRel, k) < lbRel) run = false;

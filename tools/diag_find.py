@@ -32,7 +32,7 @@ assert lib.sz4_diag_read(buf.ctypes.data, buf.size) == 0
 d = buf.reshape(-1, 8).astype(np.float64)
 cyc = d[:, 1] - d[:, 0]
 print(f"waves {nwaves}: below-chunk steps dB {d[:, 2].sum():.4g}, shift steps dL {d[:, 3].sum():.4g}, "
-      f"improve dBi {d[:, 4].sum():.4g}, extension steps dLi {d[:, 5].sum():.4g}")
+      f"broadcast steps serving <= 32 lanes {d[:, 4].sum():.4g}, <= 8 lanes {d[:, 5].sum():.4g}")
 print(f"per wave: dB {d[:, 2].mean():.1f} dL {d[:, 3].mean():.1f}; cycles mean {cyc.mean():.4g} max {cyc.max():.4g}")
 t_entry, t_search = d[:, 6], d[:, 7]
 ok = t_entry > 0
