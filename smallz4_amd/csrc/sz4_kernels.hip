@@ -2871,8 +2871,9 @@ struct LazyWalker {
   uint32_t wbase, wL, xL1, xL2, xL3;
   __device__ __forceinline__ uint32_t ldw(uint32_t b) const
   {
-    const uint32_t lane = lane_id();
-    return b + lane <= lastSearch ? L[b + lane] : 0u;
+    // unconditional load (clamped index; masked in next()): see k_walk
+    const uint32_t i = b + lane_id();
+    return L[i <= lastSearch ? i : lastSearch];
   }
   __device__ __forceinline__ void start(uint32_t pos)
   {
@@ -2897,7 +2898,7 @@ struct LazyWalker {
           start(pos);
         }
       }
-      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch) & (~0ull << (pos - wbase));
+      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch && wbase + lane_id() <= lastSearch) & (~0ull << (pos - wbase));
       const uint32_t pc = (uint32_t)__popcll(mask);
       if (need < pc) {
         // the set bit with exactly `need` set bits below it: each lane counts its own (mbcnt)
@@ -3733,10 +3734,16 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   const uint32_t a = ws.y * kWalkSeg;
   const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
 
-  uint32_t pos = a, wbase = a, m = 0;
+  uint32_t pos = a, wbase = a, m = 0, slotBuf = 0;
   bool viaMatch = false;
   uint32_t wL, xL1, xL2, xL3;
-  auto ldw = [&](uint32_t b) -> uint32_t { return b + lane < n ? L[b + lane] : 0u; };
+  // unconditional loads (the index clamped; lanes past the block are masked where the window is
+  // used): a load under a branch, or a value masked right after it, makes the compiler wait for the
+  // load before the window is used, which defeats the prefetch
+  auto ldw = [&](uint32_t b) -> uint32_t {
+    const uint32_t i = b + lane;
+    return L[i < n ? i : n - 1u];
+  };
   wL = ldw(a);
   xL1 = ldw(a + 64);
   xL2 = ldw(a + 128);
@@ -3758,7 +3765,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
       }
     }
     const uint32_t rel = pos - wbase;
-    const uint64_t mm = __ballot(wL > 1u) & (~0ull << rel);
+    const uint64_t mm = __ballot(wL > 1u && wbase + lane < n) & (~0ull << rel);
     const uint32_t q = mm ? wbase + (uint32_t)__builtin_ctzll(mm) : wbase + 64;  // next match (or window end)
     if (q >= aNext) {
       viaMatch = false;  // literals carry the path to aNext itself
@@ -3774,11 +3781,14 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
       if (lane == 0) atomicOr(status, kStInvariant);
       break;
     }
-    if (lane == 0) slots[m] = q;
+    // match positions collect in a register (lane m mod 64) and leave 64 at a time, coalesced
+    slotBuf = wrlane(slotBuf, q, m & 63u);
     m++;
+    if ((m & 63u) == 0u) slots[m - 64u + lane] = slotBuf;
     pos = q + rdlane(wL, q - wbase);
     viaMatch = true;
   }
+  if (lane < (m & 63u)) slots[(m & ~63u) + lane] = slotBuf;
   if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, viaMatch ? pos : aNext, 0u);
 }
 
