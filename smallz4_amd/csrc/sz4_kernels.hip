@@ -799,6 +799,9 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
     // slot itself is not a target (window-only positions)
     const bool inChunk = lane < count;
     const uint32_t myRel = inChunk ? slot_pos(compact, small, slot) : 0u;
+    // the first block of candidates below the chunk (slots first - 1 - lane), loaded with the chunk's own
+    // slots: a load issued later, before the in-chunk walk, made the compiler wait for it right there
+    const uint32_t belowPre = slot_pos(compact, small, first > lane ? first - 1u - lane : 0u);
     const uint32_t gs = inChunk ? slot_gs(compact, small, E, slot) : slot;
     const uint64_t p = S.w0 + myRel;
     const uint32_t me0 = inChunk ? src.ld4(p) : 0u, me1 = inChunk ? src.ld4(p + 4) : 0u;
@@ -1009,7 +1012,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       if (__ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
         int32_t cBase = (int32_t)first - 1;
-        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? slot_pos(compact, small, (uint32_t)(cBase - (int32_t)lane)) : 0u;
+        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? belowPre : 0u;
         while (cBase >= gsB && __ballot(run)) {
           uint32_t fRel;
           asm volatile("v_mov_b32 %0, %1" : "=v"(fRel) : "v"(nextBlk));
@@ -1101,7 +1104,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       if (__ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
         int32_t cBase = (int32_t)first - 1;
-        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? slot_pos(compact, small, (uint32_t)(cBase - (int32_t)lane)) : 0u;
+        uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? belowPre : 0u;
         while (cBase >= gsB && __ballot(run)) {
           uint32_t fRel;
           asm volatile("v_mov_b32 %0, %1" : "=v"(fRel) : "v"(nextBlk));
