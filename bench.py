@@ -375,10 +375,10 @@ def main():
                "bytes_per_gpu": nbytes, "parallelism": f"block ranges of one input sharded over {world} GPU(s), "
                                                       "no data-path collective"}
         # dominant kernel k_find_sorted (the sort fused in).  Algorithmic bytes per position: text byte
-        # (1) + the sorted slot arrays written and read back (4 + 4: u16 position and group start) +
-        # the match written (6: u32 length, u16 distance) = 15 B
+        # read (1) + the sorted slot arrays written for the later passes (4: u16 position and group
+        # start) + the match written (6: u32 length, u16 distance) = 11 B
         find_ms = stages.get("find_sorted", 0.0)
-        alg_bytes = 15 * nbytes
+        alg_bytes = 11 * nbytes
         achieved = alg_bytes / (find_ms * 1e-3) / 1e9 if find_ms > 0 else 0.0
         pmc_cfg = {"workload": args.workload, "bytes_per_gpu": nbytes, "block_size": bs, "level": args.level}
         pmc = pmc_traffic(pmc_cfg)
