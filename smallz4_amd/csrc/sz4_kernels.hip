@@ -944,11 +944,28 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       };
       // 1. inside the chunk: shift register (after s shifts lane l holds slot first + l - s)
 #if SZ4_LEAN_SHIFT
-      if (!needWin) {
-        // no window test: lane l has slot - max(gs, first) candidates inside the chunk, so the walk is
-        // a uniform trip count (the longest of them) with a per-lane bound -- no per-step walk flags
+      {
+        // lane l has slot - max(gs, first) candidates inside the chunk (lanes below it), so the walk is a
+        // uniform trip count (the longest of them) with a per-lane bound -- no per-step walk flags.  With a
+        // window test the bound starts at the lowest of those lanes inside the window (positions ascend
+        // with the lane inside a group: a binary search over the chunk), and a lane cut by the window has
+        // nothing left below the chunk
         const int32_t lo1 = (int32_t)(gs > first ? gs : first);
-        const uint32_t myCnt = run && (int32_t)slot > lo1 ? (uint32_t)((int32_t)slot - lo1) : 0u;
+        uint32_t jLo = run && (int32_t)slot > lo1 ? (uint32_t)(lo1 - (int32_t)first) : lane;
+        if (needWin) {
+          uint32_t a = jLo, b = lane;  // the first lane j in [a, b) with myRel(j) >= lbRel, else b
+#pragma unroll
+          for (int it = 0; it < 6; it++) {
+            const uint32_t mid = (a + b) >> 1;
+            const uint32_t rj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mid << 2), (int)myRel);
+            const bool go = a < b;
+            if (go && rj < lbRel) a = mid + 1u;
+            else if (go) b = mid;
+          }
+          if (a > jLo) run = false;
+          jLo = a;
+        }
+        const uint32_t myCnt = lane - jLo;
         const uint32_t rm = row_max(myCnt);
         const uint32_t trips = max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
         uint32_t r0 = me0, r1 = me1, r2 = me2;
@@ -985,8 +1002,8 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
           visit(s <= myCnt, slot - s, r0, r1, r2);
         }
         run = run && (int32_t)gs < (int32_t)first;
-      } else
-#endif
+      }
+#else
       {
         const int32_t lo1 = (int32_t)(gs > first ? gs : first);
         uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
@@ -1008,6 +1025,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         }
         run = run && (int32_t)gs < (int32_t)first;
       }
+#endif
       // 2. below the chunk: the group that started before it, one uniform candidate per step
       if (__ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
