@@ -1048,10 +1048,21 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
           }
 #endif
           if (needWin) {
-            for (int32_t k = 0; k < n; k++) {
-              if (run && rdlane(fRel, k) < lbRel) run = false;
-              visit(run, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+            // the block's candidates inside this lane's window: positions descend with k, so they are
+            // the first kc (a binary search over the block); a lane whose window ends here is done
+            uint32_t a = 0, b = (uint32_t)n;  // up to 64 candidates: 7 halvings
+#pragma unroll
+            for (int it = 0; it < 7; it++) {
+              const uint32_t mid = (a + b) >> 1;
+              const uint32_t fk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mid << 2), (int)fRel);
+              const bool go = a < b;
+              if (go && fk >= lbRel) a = mid + 1u;
+              else if (go) b = mid;
             }
+            const uint32_t kc = run ? a : 0u;
+            for (int32_t k = 0; k < n; k++)
+              visit((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+            if (kc < (uint32_t)n) run = false;
           } else {
             // no window test: every lane may take the candidate (only the group's lanes can match; a
             // lane finished at its cap cannot move: its queued candidates never beat the one it has)
