@@ -914,6 +914,16 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         bestKey = key > bestKey ? key : bestKey;
         return x0 | x1 | x2;
       };
+      // score() for the lanes where `mine` holds (nonzero for the others)
+      auto scoreIf = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
+        const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        const uint32_t lcp = min(4u + (z >> 3), cap12);
+        const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+        return mine ? x0 | x1 | x2 : 1u;
+      };
       // queue the lanes of `sat` (12 bytes equal, may grow past them) with candidate slot cs
       auto enqueue = [&](uint64_t sat, uint32_t cs) {
         if (sat) {
@@ -1060,7 +1070,17 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
               else if (go) b = mid;
             }
             const uint32_t kc = run ? a : 0u;
-            for (int32_t k = 0; k < n; k++)
+            int32_t k = 0;
+            for (; k + 1 < n; k += 2) {
+              const uint32_t xa = scoreIf((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              const uint32_t xb = scoreIf((uint32_t)k + 1u < kc, (uint32_t)(cBase - k - 1), rdlane(f0, k + 1),
+                                          rdlane(f1, k + 1), rdlane(f2, k + 1));
+              if (__ballot(min(xa, xb) == 0u) & satOk) {
+                enqueue(__ballot(xa == 0u) & satOk, (uint32_t)(cBase - k));
+                enqueue(__ballot(xb == 0u) & satOk, (uint32_t)(cBase - k - 1));
+              }
+            }
+            if (k < n)
               visit((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             if (kc < (uint32_t)n) run = false;
           } else {
