@@ -32,6 +32,18 @@
 #ifndef SZ4_SHIFT_UNROLL
 #define SZ4_SHIFT_UNROLL 1
 #endif
+#ifndef SZ4_SKIP_SHIFT  // timing experiments only (results wrong): leave out a phase of k_find_sorted
+#define SZ4_SKIP_SHIFT 0
+#endif
+#ifndef SZ4_SKIP_BCAST
+#define SZ4_SKIP_BCAST 0
+#endif
+#ifndef SZ4_SKIP_SEARCH
+#define SZ4_SKIP_SEARCH 0
+#endif
+#ifndef SZ4_FILTER
+#define SZ4_FILTER 1  // -9: candidates pass a strict-improvement mask test first, the exact prefix only on a hit
+#endif
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
@@ -785,7 +797,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
   const bool unlimited = maxChain >= 65535u;
   // every distance inside a segment of at most 64 KiB is in the window, unless the lookback cut applies
   const bool needWin = (S.s1 - S.w0 > 65536u) || cut != kNone;
-  const uint32_t nChunks = (E + 63) / 64;
+  const uint32_t nChunks = SZ4_SKIP_SEARCH ? 0u : (E + 63) / 64;
 
   while (true) {
     uint32_t item = 0;
@@ -952,6 +964,26 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
           if (qn >= 64) flush();
         }
       };
+#if SZ4_FILTER
+      // candidates arrive nearest first (slots descend), so one can raise bestKey only with a longer
+      // prefix: it must match the first bestLen + 1 bytes (all 12 once a lane holds 12 or its cap).
+      // m1 / m2 mask bytes 4..11 of that need; the exact prefix is computed on a hit only
+      auto setMasks = [&]() {
+        const uint32_t len = bestKey >> 17;
+        const uint32_t need = len >= cap12 ? 12u : len + 1u;
+        m1 = need >= 8u ? ~0u : need > 4u ? (1u << (8u * (need - 4u))) - 1u : 0u;
+        m2 = need >= 12u ? ~0u : need > 8u ? (1u << (8u * (need - 8u))) - 1u : 0u;
+      };
+      auto filt = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
+        return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
+      };
+      auto hit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
+        const uint32_t x = scoreIf(mine, cs, k0, k1, k2);
+        setMasks();
+        enqueue(__ballot(x == 0u) & satOk, cs);
+      };
+      setMasks();
+#endif
       // 1. inside the chunk: shift register (after s shifts lane l holds slot first + l - s)
 #if SZ4_LEAN_SHIFT
       {
@@ -977,10 +1009,40 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
         }
         const uint32_t myCnt = lane - jLo;
         const uint32_t rm = row_max(myCnt);
-        const uint32_t trips = max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
+        const uint32_t trips = SZ4_SKIP_SHIFT ? 0u : max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
         uint32_t r0 = me0, r1 = me1, r2 = me2;
         uint32_t s = 1;
-#if SZ4_SHIFT_UNROLL
+#if SZ4_FILTER
+        // wave shift right by one, zero into lane 0 (bound_ctrl: no old value to set up)
+        auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kWaveShr1, 0xF, 0xF, true); };
+        if (!needWin) {
+          // a source lane below the target's group holds another key (x0 != 0), so only the lanes that do
+          // not run need a mask, folded into the first word's test
+          const uint32_t dead = run ? 0u : ~0u;
+          for (; s <= trips; s++) {
+#if SZ4_DIAG == 3
+            dL++;
+#endif
+            r0 = shr1(r0);
+            r1 = shr1(r1);
+            r2 = shr1(r2);
+            const uint32_t y = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
+            if (__ballot(y == 0u)) hit(s <= myCnt, slot - s, r0, r1, r2);
+          }
+        } else {
+          for (; s <= trips; s++) {
+#if SZ4_DIAG == 3
+            dL++;
+#endif
+            r0 = shr1(r0);
+            r1 = shr1(r1);
+            r2 = shr1(r2);
+            const uint32_t dead = s <= myCnt ? 0u : ~0u;
+            const uint32_t y = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
+            if (__ballot(y == 0u)) hit(s <= myCnt, slot - s, r0, r1, r2);
+          }
+        }
+#elif SZ4_SHIFT_UNROLL
         // two shifts per step, one saturation test for the two (four would exceed 64 VGPRs: 8 waves/SIMD)
         for (; s + 1 <= trips; s += 2) {
 #if SZ4_DIAG == 3
@@ -1037,7 +1099,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
       }
 #endif
       // 2. below the chunk: the group that started before it, one uniform candidate per step
-      if (__ballot(run)) {
+      if (!SZ4_SKIP_BCAST && __ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
         int32_t cBase = (int32_t)first - 1;
         uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? belowPre : 0u;
@@ -1071,6 +1133,12 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
             }
             const uint32_t kc = run ? a : 0u;
             int32_t k = 0;
+#if SZ4_FILTER
+            for (; k < n; k++) {
+              const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
+              if (__ballot((uint32_t)k < kc && filt(k0, k1, k2) == 0u)) hit((uint32_t)k < kc, (uint32_t)(cBase - k), k0, k1, k2);
+            }
+#endif
             for (; k + 1 < n; k += 2) {
               const uint32_t xa = scoreIf((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
               const uint32_t xb = scoreIf((uint32_t)k + 1u < kc, (uint32_t)(cBase - k - 1), rdlane(f0, k + 1),
@@ -1087,6 +1155,15 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
             // no window test: every lane may take the candidate (only the group's lanes can match; a
             // lane finished at its cap cannot move: its queued candidates never beat the one it has)
             int32_t k = 0;
+#if SZ4_FILTER
+            for (; k < n; k++) {
+#if SZ4_DIAG == 3
+              dB++;
+#endif
+              const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
+              if (__ballot(filt(k0, k1, k2) == 0u)) hit(true, (uint32_t)(cBase - k), k0, k1, k2);
+            }
+#endif
             for (; k + 1 < n; k += 2) {
 #if SZ4_DIAG == 3
               dB += 2;
