@@ -707,13 +707,12 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 }
 
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96))) void k_find_sorted(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
-                                                              const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
-                                                              const uint32_t* __restrict__ ivCount, uint2* compactAll,
-                                                              uint32_t maxChain, uint32_t* __restrict__ mlen,
-                                                              uint16_t* __restrict__ mdist, uint64_t matchBase,
-                                                              uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong,
-                                                              uint2* sortA, uint32_t* rankOut, uint32_t fuseSort)
+__device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
+                                uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
+                                uint32_t* rankOut, uint32_t fuseSort)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
@@ -1349,6 +1348,28 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96)
     d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = tEntry; d[7] = tSearch;
   }
 #endif
+}
+
+// two 16-wave workgroups per CU need 8 waves per SIMD: .sgpr_count <= 80 (800 SGPRs per SIMD, a wave takes
+// ceil(sgpr / 16) * 16 + 16; 82..96 admits 7 and so only one such workgroup).  Without the whole window
+// in LDS a workgroup stages up to 128 KiB and runs alone on its CU: there the spills would only cost
+__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(80))) void k_find_sorted_lds(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
+                                uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
+                                uint32_t* rankOut, uint32_t fuseSort)
+{
+  find_sorted_body<true>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
+}
+__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96))) void k_find_sorted_hbm(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+                                const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
+                                uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
+                                uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
+                                uint32_t* rankOut, uint32_t fuseSort)
+{
+  find_sorted_body<false>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
 }
 
 template <bool kLds>
@@ -4329,11 +4350,11 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
   if (ldsWindow) {
     // dynamic-LDS limits are per function and device: set them on every launch (a host-side call,
     // no synchronisation) rather than caching them process-wide
-    const void* fn = pass == 1 ? (const void*)k_find_sorted<true>
+    const void* fn = pass == 1 ? (const void*)k_find_sorted_lds
                      : unlimited ? (const void*)k_find_long9<true> : (const void*)k_find<true>;
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
     if (pass == 1)
-      hipLaunchKernelGGL(k_find_sorted<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
+      hipLaunchKernelGGL(k_find_sorted_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                          ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank,
                          (uint32_t)fuseSort);
     else if (unlimited) {
@@ -4354,8 +4375,8 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     if (pass == 1) {
       // the sort and the text-order result tiles use the same buffer: at least 64 KiB
       const uint32_t lds = hybridLds > kOutTile * 4u ? hybridLds : kOutTile * 4u;
-      hipFuncSetAttribute((const void*)k_find_sorted<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL(k_find_sorted<false>, dim3(nsegs), dim3(kFindThreads), lds, s, in, segs, blocks, iv, ivCount,
+      hipFuncSetAttribute((const void*)k_find_sorted_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(k_find_sorted_hbm, dim3(nsegs), dim3(kFindThreads), lds, s, in, segs, blocks, iv, ivCount,
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {
