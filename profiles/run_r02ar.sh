@@ -1,0 +1,16 @@
+# round 2: flush extends only candidates that can beat the best; masks by one 64-bit shift (4 MiB blocks, stream blocks with the lookback cut) -- A/B on 64 KiB and 4 MiB blocks, parity
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/r02ar
+mkdir -p $OUT
+A="--no-verify --no-decode --no-stream --cpu-seconds 0.2 --steps 5 --warmup 2"
+L=$GRAFT_REPO_ROOT/smallz4_amd/lib
+for rep in 1 2; do
+  for v in old new; do
+    if [ $v = new ]; then lib=$L/libsmallz4_amd.so; else lib=$L/libsmallz4_amd_$v.so; fi
+    SMALLZ4_AMD_LIB=$lib timeout -k 10 120 python -u bench.py $A > $OUT/ab_${v}_$rep.json 2> $OUT/ab_${v}_$rep.err || exit 1
+    SMALLZ4_AMD_LIB=$lib timeout -k 10 120 python -u bench.py $A --block-size 4194304 --mb 64 > $OUT/ab4m_${v}_$rep.json 2> $OUT/ab4m_${v}_$rep.err || exit 1
+  done
+done
+timeout -k 10 700 python -u -m pytest tests/test_gpu.py tests/test_stream.py -x -v --timeout 170 --timeout-method thread -k "every_level or shapes or edge_sizes or other_block_sizes or silesia or structured or stream_multiblock or golden or run_across or chunk_boundaries or long_matches or finder_intermediate" > $OUT/tests.log 2>&1
+timeout -k 10 200 python -u tools/diag_find.py 100 > $OUT/diag.txt 2>&1

@@ -44,6 +44,12 @@
 #ifndef SZ4_FILTER
 #define SZ4_FILTER 1  // -9: candidates pass a strict-improvement mask test first, the exact prefix only on a hit
 #endif
+#ifndef SZ4_SAT_THRESHOLD
+#define SZ4_SAT_THRESHOLD 1  // -9 flush: a queued candidate is extended only if it can beat the target's best
+#endif
+#ifndef SZ4_FILTER_UNROLL
+#define SZ4_FILTER_UNROLL 0  // two candidates per hit test in the filtered loops (neutral at one workgroup per CU)
+#endif
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
@@ -888,6 +894,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       auto flush = [&]() {
         // lane t extends queue entry base + t: target = lane (e >> 17), candidate slot e & 0x1FFFF
         for (uint32_t base = 0; base < qn; base += 64) {
+#if SZ4_DIAG == 3
+        dLi += 1ull << 30;  // flush rounds
+#endif
         const uint32_t e = base + lane < qn ? satQ[base + lane] : 0u;
         const uint32_t tl = e >> 17, cs = e & 0x1FFFFu;
         const uint32_t tRel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)myRel);
@@ -896,7 +905,19 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const uint64_t tp = S.w0 + tRel, cp = S.w0 + slot_pos(compact, small, cs);
           uint32_t kk = 12;
           bool open = true;
+#if SZ4_SAT_THRESHOLD
+          // queued after the target's best so far (nearest first), so it only counts if longer: it
+          // must match byte `cur` (one 4-byte test) before it is extended
+          const uint32_t cur = satBest[tl] >> 17;
+          if (cur >= 12u && (cur >= tLim || src.ld4(tp + cur - 3) != src.ld4(cp + cur - 3))) {
+            open = false;
+            kk = 0;
+          }
+#endif
           while (open && kk < tLim) {
+#if SZ4_DIAG == 3
+            dLi++;  // lane-steps of the saturated extension
+#endif
             const uint32_t x = src.ld4(tp + kk) ^ src.ld4(cp + kk);
             if (x) {
               kk += (uint32_t)__builtin_ctz(x) >> 3;
@@ -906,7 +927,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             }
           }
           if (kk > tLim) kk = tLim;
-          atomicMax(&satBest[tl], (kk << 17) | cs);
+          if (kk) atomicMax(&satBest[tl], (kk << 17) | cs);
         }
         }
         qn = 0;
@@ -969,14 +990,18 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // m1 / m2 mask bytes 4..11 of that need; the exact prefix is computed on a hit only
       auto setMasks = [&]() {
         const uint32_t len = bestKey >> 17;
-        const uint32_t need = len >= cap12 ? 12u : len + 1u;
-        m1 = need >= 8u ? ~0u : need > 4u ? (1u << (8u * (need - 4u))) - 1u : 0u;
-        m2 = need >= 12u ? ~0u : need > 8u ? (1u << (8u * (need - 8u))) - 1u : 0u;
+        const uint32_t need = len >= cap12 ? 12u : max(len + 1u, 4u);  // 4..12
+        const uint64_t mk = need >= 12u ? ~0ull : (1ull << (8u * (need - 4u))) - 1ull;
+        m1 = (uint32_t)mk;
+        m2 = (uint32_t)(mk >> 32);
       };
       auto filt = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
         return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
       };
       auto hit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
+#if SZ4_DIAG == 3
+        dBi++;  // hit branches (wave-level)
+#endif
         const uint32_t x = scoreIf(mine, cs, k0, k1, k2);
         setMasks();
         enqueue(__ballot(x == 0u) & satOk, cs);
@@ -1018,6 +1043,27 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           // a source lane below the target's group holds another key (x0 != 0), so only the lanes that do
           // not run need a mask, folded into the first word's test
           const uint32_t dead = run ? 0u : ~0u;
+#if SZ4_FILTER_UNROLL
+          // two shifts per test (a hit keeps the first candidate's words)
+          for (; s + 1 <= trips; s += 2) {
+#if SZ4_DIAG == 3
+            dL += 2;
+#endif
+            r0 = shr1(r0);
+            r1 = shr1(r1);
+            r2 = shr1(r2);
+            const uint32_t ya = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
+            const uint32_t q0 = r0, q1 = r1, q2 = r2;
+            r0 = shr1(r0);
+            r1 = shr1(r1);
+            r2 = shr1(r2);
+            const uint32_t yb = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
+            if (__ballot(min(ya, yb) == 0u)) {
+              if (__ballot(ya == 0u)) hit(s <= myCnt, slot - s, q0, q1, q2);
+              if (__ballot(yb == 0u)) hit(s + 1u <= myCnt, slot - s - 1u, r0, r1, r2);
+            }
+          }
+#endif
           for (; s <= trips; s++) {
 #if SZ4_DIAG == 3
             dL++;
@@ -1111,12 +1157,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
 #if SZ4_DIAG == 3
-          {
-            // broadcast steps that serve at most 32 / at most 8 of the chunk's lanes
-            const uint32_t nr = (uint32_t)__builtin_popcountll(__ballot(run));
-            if (nr <= 32u) dBi += (uint64_t)n;
-            if (nr <= 8u) dLi += (uint64_t)n;
-          }
+          dLi += 1ull << 46;  // broadcast blocks
 #endif
           if (needWin) {
             // the block's candidates inside this lane's window: positions descend with k, so they are
@@ -1155,6 +1196,20 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             // lane finished at its cap cannot move: its queued candidates never beat the one it has)
             int32_t k = 0;
 #if SZ4_FILTER
+#if SZ4_FILTER_UNROLL
+            for (; k + 1 < n; k += 2) {
+#if SZ4_DIAG == 3
+              dB += 2;
+#endif
+              const uint32_t a0 = rdlane(f0, k), a1 = rdlane(f1, k), a2 = rdlane(f2, k);
+              const uint32_t b0 = rdlane(f0, k + 1), b1 = rdlane(f1, k + 1), b2 = rdlane(f2, k + 1);
+              const uint32_t ya = filt(a0, a1, a2), yb = filt(b0, b1, b2);
+              if (__ballot(min(ya, yb) == 0u)) {
+                if (__ballot(ya == 0u)) hit(true, (uint32_t)(cBase - k), a0, a1, a2);
+                if (__ballot(yb == 0u)) hit(true, (uint32_t)(cBase - k - 1), b0, b1, b2);
+              }
+            }
+#endif
             for (; k < n; k++) {
 #if SZ4_DIAG == 3
               dB++;
@@ -1343,6 +1398,11 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #if SZ4_DIAG == 3
   const uint64_t t2 = __builtin_readcyclecounter();
   const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
+  {
+    uint64_t sLo = 0;
+    for (int l = 0; l < 64; l++) sLo += (uint64_t)__shfl((long long)(dLi & 0x3FFFFFFFull), l);
+    dLi = (dLi & ~0x3FFFFFFFull) | sLo;
+  }
   if (lane == 0 && w * 8 + 8 <= (1u << 20)) {
     uint64_t* d = sz4_diag + w * 8;
     d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = tEntry; d[7] = tSearch;

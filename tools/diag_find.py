@@ -41,3 +41,4 @@ print(f"phases per wave (ticks): sort {(d[ok, 0] - t_entry[ok]).mean():.4g}, "
       f"window load + search {(t_search[ok] - d[ok, 0]).mean():.4g}, text-order output {(d[ok, 1] - t_search[ok]).mean():.4g}; "
       f"kernel span {span:.4g} ticks in {find_ms:.3f} ms -> {span / find_ms / 1e6:.3f} GHz")
 print(f"per position: dB {d[:, 2].sum() / n:.3f} dL {d[:, 3].sum() / n:.3f} (wave-steps per target position)")
+print(f"hit branches per position {d[:, 4].sum() / n:.3f}; broadcast blocks {(buf.reshape(-1, 8)[:, 5] >> np.uint64(46)).sum() / n:.4f}/pos, flush rounds {((buf.reshape(-1, 8)[:, 5] >> np.uint64(30)) & np.uint64(0xFFFF)).sum() / n:.4f}/pos, extension lane-steps {(buf.reshape(-1, 8)[:, 5] & np.uint64(0x3FFFFFFF)).sum() / n:.3f}/pos")
