@@ -129,6 +129,7 @@ struct sz4_ctx {
 
   DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
+  DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf chunkOut;             // stream path: one chunk's blocks
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
@@ -169,7 +170,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
             &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut, &unSeq};
   }
 
@@ -235,7 +236,14 @@ void finish_plan(sz4_ctx* c)
     B.dpCount = 0;
     if (n <= (uint64_t)kTailNoMatch) continue;
     const uint64_t top = n - 1 - kTailLiterals;
-    const uint64_t seg = dp_segment_size(n);
+    uint64_t seg = dp_segment_size(n);
+    if (n > 65536) {
+      // tuning knob for blocks above 64 KiB: a multiple of 256 (the parse's range-minimum blocks)
+      if (const char* e = getenv("SZ4_DP_SIZE")) {
+        const uint64_t v = strtoull(e, nullptr, 10);
+        if (v >= 1024 && v % 256 == 0 && (n + v - 1) / v <= kMaxDpSegs) seg = v;
+      }
+    }
     B.dpSize = (uint32_t)seg;
     for (uint64_t hi = top, k = 0;; hi -= seg, k++) {
       const uint64_t lo = hi + 1 >= seg ? hi + 1 - seg : 0;
@@ -277,6 +285,8 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->sel.reserve(stagedBytes * 4 + 64)) ||
       (e = c->reach.reserve(stagedBytes * 4 + 64)) ||
       (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
+      (e = c->dpSide.reserve(c->hDp.size() * dp_side_positions() * sizeof(uint2) + 64)) ||
+      (e = c->dpRec.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
       (e = c->walkSegs.reserve(c->hWalk.size() * sizeof(uint2) + 64)) ||
       (e = c->walkSlots.reserve(c->hWalk.size() * 2 * kWalkCap * 4 + 64)) ||
       (e = c->walkState.reserve(c->hWalk.size() * sizeof(uint4) + 64)) ||
@@ -391,6 +401,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
                c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp.as<uint32_t>(), c->rmqDown.as<uint32_t>(),
+               c->dpSide.as<uint2>(), c->dpRec.as<uint4>(),
                c->status.as<int>(), s);
   mark(c, 5, s);
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");

@@ -70,10 +70,10 @@ struct DpSeg {
   uint32_t k;              // 0 = the segment holding the block's last parsed position
   uint32_t lo, hi;         // block-relative positions [lo, hi], parsed from hi down
 };
-// short segments give more parallelism; the repair pass walks a block's boundaries one after the
-// other, so large blocks keep longer segments
-inline uint32_t dp_segment_size(uint64_t n) { return n <= 65536 ? 4096u : 16384u; }
-constexpr uint32_t kMaxDpSegs = 512;  // 8 MiB legacy block / 16384
+// short segments give more parallelism; the serial part of the repair (k_dp_fix<false>) walks a
+// block's boundaries one after the other, so large blocks keep longer segments
+inline uint32_t dp_segment_size(uint64_t n) { return n <= 65536 ? 4096u : 8192u; }
+constexpr uint32_t kMaxDpSegs = 2048;  // 8 MiB legacy block / 4096 (SZ4_DP_SIZE)
 
 // the token walk runs as sub-segments of kWalkSeg positions, each walked speculatively from its
 // first position and repaired by k_walk_fix; a sub-segment's match positions live in 2 * kWalkCap
@@ -128,7 +128,10 @@ uint32_t lazy_slots_per_walk();
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,
-                  const uint32_t* longFlag, uint32_t* rmqUp, uint32_t* rmqDown, int* status, hipStream_t s);
+                  const uint32_t* longFlag, uint32_t* rmqUp, uint32_t* rmqDown, uint2* dpSide, uint4* dpRec, int* status,
+                  hipStream_t s);
+// k_dp_fix<true>'s saved speculative values: dp_side_positions() uint2 per DpSeg, and one uint4 record per DpSeg
+uint32_t dp_side_positions();
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
                  uint32_t maxChain, const uint32_t* chosen, const uint16_t* mdist, uint64_t matchBase, uint32_t* walkSlots,
                  uint4* walkState, uint32_t* posList, Token* tokens, uint32_t* ntok, uint32_t* blockBytes,

@@ -3634,18 +3634,48 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, 0u, 0u);
 }
 
+// k_dp_fix<true>: the repair of every segment k >= 1 of a block without range minima at once, each from
+// the SPECULATIVE costs and state of segment k - 1 (one wavefront per segment).  Choices depend on cost
+// differences only, so the result is exact whenever everything it read lies in the part of k - 1 that
+// k - 1's own (true) repair left speculative -- below k - 1's convergence point -- and k - 1 converged:
+// its costs are then the exact ones minus that part's offset.  It saves the speculative values it
+// overwrites (side, kDpSide positions at most, or it gives up) and records (conv or lowest position
+// written, cost delta at conv, highest position read above the segment, converged) in dpRec.
+// k_dp_fix<false> (one wavefront per block) then walks the boundaries: a segment whose record is exact
+// only enters the offset tables; the others get their speculative values back and are repaired
+// serially as before.
+constexpr uint32_t kDpSide = 512;
+
+template <bool kPar>
 __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
-                                               const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                               uint32_t ndp, const uint32_t* __restrict__ mlen,
+                                               const uint16_t* __restrict__ mdist,
                                                uint64_t matchBase, uint32_t* __restrict__ costAll,
                                                uint32_t* __restrict__ sel, const uint32_t* __restrict__ reach,
                                                uint4* __restrict__ segState, const uint32_t* __restrict__ longFlag,
-                                               uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll)
+                                               uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll,
+                                               uint2* __restrict__ side, uint4* __restrict__ dpRec)
 {
   __shared__ uint32_t ring[kRing];
-  __shared__ uint32_t convTab[kMaxDpSegs];   // positions >= convTab[k] of segment k hold exact costs
-  __shared__ uint32_t deltaTab[kMaxDpSegs];  // below it: exact = stored + deltaTab[k]
-  __shared__ uint32_t convBlk[kMaxDpSegs];   // UP/DOWN keys of positions below it: exact = key cost + deltaTab[k]
-  const Block B = blocks[blockIdx.x];
+  constexpr uint32_t kTab = kPar ? 1u : kMaxDpSegs;
+  __shared__ uint32_t convTab[kTab];   // positions >= convTab[k] of segment k: exact = stored + aboveTab[k]
+  __shared__ uint32_t deltaTab[kTab];  // below it: exact = stored + deltaTab[k]
+  __shared__ uint32_t convBlk[kTab];   // UP/DOWN keys of positions below it: exact = key cost + deltaTab[k]
+  __shared__ uint32_t aboveTab[kTab];  // 0, or the offset of the segment above when k_dp_fix<true> repaired it
+  uint32_t bIdx, kFirst, kEnd;
+  if constexpr (kPar) {
+    if (blockIdx.x >= ndp) return;
+    const DpSeg G0 = dpSegs[blockIdx.x];
+    if (G0.k == 0 || (longFlag[G0.block] & kFlagRmq)) return;
+    bIdx = G0.block;
+    kFirst = G0.k;
+    kEnd = G0.k + 1;
+  } else {
+    bIdx = blockIdx.x;
+    kFirst = 1;
+    kEnd = blocks[bIdx].dpCount;
+  }
+  const Block B = blocks[bIdx];
   if (B.dpCount <= 1) return;
   const uint32_t lane = threadIdx.x;
   const uint64_t base = B.start - matchBase;
@@ -3656,26 +3686,68 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   uint32_t* S = sel + base;
   const uint32_t first = dpSegs[B.dpFirst].hi;  // n - 6: the last parsed position
   const int32_t top = (int32_t)first;
-  const bool rmq = (longFlag[blockIdx.x] & kFlagRmq) != 0u;
+  const bool rmq = kPar ? false : (longFlag[bIdx] & kFlagRmq) != 0u;
   uint32_t* up = upAll + base;
   uint32_t* down = downAll + base;
-  if (lane == 0) {
+  if (!kPar && lane == 0) {
     convTab[0] = 0;  // the top segment was parsed exactly
     deltaTab[0] = 0;
     convBlk[0] = 0;
+    aboveTab[0] = 0;
   }
   __syncthreads();
-  // exact cost of a position above the segment being repaired (0 past the parsed range)
+  // exact cost of a position above the segment being repaired (0 past the parsed range); k_dp_fix<true>
+  // takes the stored (speculative) costs, exact up to one offset where its result is used
   auto exact_above = [&](uint32_t j) -> uint32_t {
     if (j > first) return 0u;
-    const uint32_t k = (first - j) / B.dpSize;
-    const uint32_t v = ld_fresh(&cost[j]);
-    return j < convTab[k] ? v + deltaTab[k] : v;
+    if constexpr (kPar) {
+      return cost[j];
+    } else {
+      const uint32_t k = (first - j) / B.dpSize;
+      const uint32_t v = ld_fresh(&cost[j]);
+      return v + (j < convTab[k] ? deltaTab[k] : aboveTab[k]);
+    }
   };
+  // k_dp_fix<false> over blocks that k_dp_fix<true> repaired: the records 64 segments at a time
+  const bool par = !kPar && !rmq;
+  uint4 recV = make_uint4(0u, 0u, 0u, 0u);
+  uint32_t prevV = 0, prevConv = 0;  // offset below segment k - 1's convergence point, that point
+  bool prevDone = true;              // segment k - 1's repair converged (segment 0 is exact)
 
-  for (uint32_t k = 1; k < B.dpCount; k++) {
+  for (uint32_t k = kFirst; k < kEnd; k++) {
     const DpSeg G = dpSegs[B.dpFirst + k];
     const int32_t lo = (int32_t)G.lo, hi = (int32_t)G.hi;
+    if (par) {
+      if (((k - 1u) & 63u) == 0u) {
+        const uint32_t kk = k + lane;
+        recV = kk < B.dpCount ? dpRec[B.dpFirst + kk] : make_uint4(0u, 0u, 0u, 0u);
+      }
+      const uint32_t t = (k - 1u) & 63u;
+      const uint32_t rConv = rdlane(recV.x, t), rDelta = rdlane(recV.y, t);
+      const uint32_t rReach = rdlane(recV.z, t), rFlag = rdlane(recV.w, t);
+      if ((rFlag & 1u) && (k == 1u || (prevDone && rReach < prevConv))) {
+        // everything it read was exact - prevV: its costs are exact - prevV
+        if (lane == 0) {
+          convTab[k] = rConv;
+          convBlk[k] = rConv;
+          aboveTab[k] = prevV;
+          deltaTab[k] = prevV + rDelta;
+        }
+        prevV += rDelta;
+        prevConv = rConv;
+        prevDone = true;
+        __syncthreads();
+        continue;
+      }
+      // repaired from a wrong state: the speculative values back, then the serial repair
+      uint2* sd = side + (uint64_t)(B.dpFirst + k) * kDpSide;
+      for (uint32_t t2 = lane; t2 <= (uint32_t)hi - rConv; t2 += 64) {
+        const uint2 v = sd[t2];
+        cost[hi - (int32_t)t2] = v.x;
+        S[hi - (int32_t)t2] = v.y;
+      }
+      __threadfence();  // the stores are complete and the L1 is invalidated before the reloads below
+    }
     const uint4 st = segState[B.dpFirst + k - 1];  // exact state below the segment above
     uint32_t lits = st.x, litBump = st.y;
     uint32_t costNext = exact_above((uint32_t)hi + 1);
@@ -3703,6 +3775,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     uint32_t closedCost = 0;  // closed-form chunk: cost at its end closedE
     int32_t closedE = 0;
     bool done = false;
+    int32_t maxReach = hi + 64;  // k_dp_fix<true>: highest position read above the segment
+    int32_t lowW = hi;           // k_dp_fix<true>: lowest position written
     // the chunk's inputs are loaded one chunk ahead (positions below are not rewritten before)
     uint32_t nL, nD, nS, nC, nR;
     auto load_chunk = [&](int32_t h) {
@@ -3728,6 +3802,11 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       if (h - 64 >= lo) load_chunk(h - 64);
       const int32_t cl = h - 63 > lo ? h - 63 : lo;
       const uint32_t cnt = (uint32_t)(h - cl + 1);
+      if constexpr (kPar) {
+        if ((uint32_t)(hi - h) >= kDpSide) break;  // gives up: k_dp_fix<false> repairs it
+        if (in) side[(uint64_t)blockIdx.x * kDpSide + (uint32_t)(hi - ip)] = make_uint2(cC, cS);
+        lowW = cl;
+      }
       if (__ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
         auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
@@ -3776,6 +3855,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                    return false;
                  }()) {
         const uint32_t cT = closedCost + len_extra((uint32_t)(closedE - ip));
+        if (closedE > maxReach) maxReach = closedE;
         if (closedE != chain.E) chain.valid = chain.pending = false;
         const uint32_t delta = cT - cC;
         uint32_t dPrev = __shfl_up(delta, 1, 64);
@@ -3810,6 +3890,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         const int32_t i = h - (int32_t)t;
         if (i < lo) break;
         const uint32_t Lk = rdlane(cL, t), Dk = rdlane(cD, t);
+        if (Lk >= (uint32_t)kMinMatch && i + (int32_t)Lk > maxReach) maxReach = i + (int32_t)Lk;
         lits++;
         uint32_t minCost = costNext + 1;
         if (lits == litBump) {
@@ -3903,14 +3984,23 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         }
       }
     }
-    if (lane == 0) {
-      if (!done || !rmq) convBlk[k] = (uint32_t)conv;
-      convTab[k] = (uint32_t)conv;
-      deltaTab[k] = convDelta;
-      // not converged: the state below the segment is this pass's own
-      if (!done) segState[B.dpFirst + k] = make_uint4(lits, litBump, 0u, 0u);
+    if constexpr (kPar) {
+      if (lane == 0)
+        dpRec[blockIdx.x] = make_uint4(done ? (uint32_t)conv : (uint32_t)lowW, convDelta, (uint32_t)maxReach, done ? 1u : 0u);
+    } else {
+      if (lane == 0) {
+        if (!done || !rmq) convBlk[k] = (uint32_t)conv;
+        convTab[k] = (uint32_t)conv;
+        deltaTab[k] = convDelta;
+        aboveTab[k] = 0;
+        // not converged: the state below the segment is this pass's own
+        if (!done) segState[B.dpFirst + k] = make_uint4(lits, litBump, 0u, 0u);
+      }
+      prevV = convDelta;
+      prevConv = (uint32_t)conv;
+      prevDone = done;
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -4002,31 +4092,29 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, viaMatch ? pos : aNext, 0u);
 }
 
-// k_walk_fix: one wavefront per block.  Sub-segment k's walk is exact when the true path enters it
-// at a position the speculative walk also visits; otherwise the path is walked again from its true
-// entry until it meets the speculative path, and the repaired matches go in front of the
-// speculative matches that survive.
-__global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ chosen,
-                                                 uint64_t matchBase, uint32_t* __restrict__ slotsAll,
-                                                 uint4* __restrict__ state, int* __restrict__ status)
-{
-  __shared__ uint32_t fix[kWalkCap];
-  const Block B = blocks[blockIdx.x];
-  const uint32_t lane = threadIdx.x;
-  const uint32_t n = (uint32_t)(B.end - B.start);
-  const uint32_t* L = chosen + (B.start - matchBase);
-  for (uint32_t k = 1; k < B.walkCount; k++) {
-    const uint32_t idx = B.walkFirst + k;
-    const uint32_t entry = state[idx - 1].z;  // exact exit of the sub-segment before
-    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
-    const uint4 st = state[idx];
-    if (entry == a) continue;
-    uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+// Sub-segment repair.  Sub-segment k's walk is exact when the true path enters it at a position the
+// speculative walk also visits; otherwise the path is walked again from its true entry until it meets
+// the speculative path, and the repaired matches go in front of the speculative matches that survive.
+// The true entry of k is the true exit of k - 1, which is the speculative exit of k - 1 whenever k - 1
+// needed no repair or its repaired path met the speculative one (almost always).  So:
+//   k_walk_fix_spec   one wavefront per sub-segment k >= 1 repairs k from k - 1's SPECULATIVE exit, all
+//                     at once; the repaired matches go to the free lower half of k's slots and a
+//                     record (final start, count, exit, the entry assumed) to `rec`;
+//   k_walk_fix_commit one wavefront per block checks the assumed entries against the true exits 64
+//                     sub-segments at a time, moves the repaired matches of every sub-segment whose
+//                     assumption held into place, and repairs the others again serially
+//                     (walk_repair) from their true entry.
+// walk_repair: the repair of sub-segment idx from `entry` (wave-uniform).  Returns the record; the
+// repaired matches are in fix[0, rec.y) (LDS).
+struct WalkRepair {
+  const uint32_t* L;
+  const uint32_t* slots;  // the sub-segment's 2 * kWalkCap slots
+  uint32_t lane;
+  __device__ __forceinline__ uint4 run(uint32_t* fix, uint32_t a, uint32_t aNext, uint4 st, uint32_t entry, int* status) const
+  {
     const uint32_t m = st.y - kWalkCap;
-    if (entry >= aNext) {
-      if (lane == 0) state[idx] = make_uint4(st.y, st.y, entry, 0u);
-      continue;
-    }
+    if (entry == a) return make_uint4(st.x, 0u, st.z, entry);
+    if (entry >= aNext) return make_uint4(st.y, 0u, entry, entry);
     // i = first speculative match at or after p (wave-parallel over 64 slots at a time)
     auto first_at = [&](uint32_t from, uint32_t p) -> uint32_t {
       for (uint32_t b = from; b < m; b += 64) {
@@ -4042,10 +4130,7 @@ __global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ block
       return pj + L[pj] > q;
     };
     uint32_t i = first_at(0, entry);
-    if (!inside(i, entry)) {
-      if (lane == 0) state[idx] = make_uint4(kWalkCap + i, st.y, st.z, 0u);
-      continue;
-    }
+    if (!inside(i, entry)) return make_uint4(kWalkCap + i, 0u, st.z, entry);
     uint32_t q = entry, f = 0;
     bool merged = false;
     while (q < aNext) {
@@ -4067,12 +4152,88 @@ __global__ __launch_bounds__(64) void k_walk_fix(const Block* __restrict__ block
         break;
       }
     }
-    __syncthreads();
     const uint32_t iMerge = merged ? i : m;
-    const uint32_t start = kWalkCap + iMerge - f;
-    for (uint32_t t = lane; t < f; t += 64) slots[start + t] = fix[t];
-    if (lane == 0) state[idx] = make_uint4(start, st.y, merged ? st.z : q, 0u);
-    __syncthreads();
+    return make_uint4(kWalkCap + iMerge - f, f, merged ? st.z : q, entry);
+  }
+};
+
+__global__ __launch_bounds__(64 * kWalkWaves) void k_walk_fix_spec(const Block* __restrict__ blocks,
+                                                                   const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                                   const uint32_t* __restrict__ chosen, uint64_t matchBase,
+                                                                   uint32_t* __restrict__ slotsAll,
+                                                                   const uint4* __restrict__ state, uint4* __restrict__ rec,
+                                                                   int* __restrict__ status)
+{
+  __shared__ uint32_t fixAll[kWalkWaves][kWalkCap];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint2 ws = walkSegs[idx];
+  if (ws.y == 0) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  const uint32_t a = ws.y * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+  uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+  const WalkRepair W{chosen + (B.start - matchBase), slots, lane};
+  uint32_t* fix = fixAll[wave];
+  // k_walk's exit of k - 1 (this kernel writes no state)
+  const uint4 r = W.run(fix, a, aNext, state[idx], state[idx - 1].z, status);
+  __builtin_amdgcn_wave_barrier();  // lane 0's fix[] stores before the other lanes read them
+  // repaired matches to the lower half [0, f): it holds nothing k_walk wrote
+  for (uint32_t t = lane; t < r.y; t += 64) slots[t] = fix[t];
+  if (lane == 0) rec[idx] = r;
+}
+
+__global__ __launch_bounds__(64) void k_walk_fix_commit(const Block* __restrict__ blocks, const uint32_t* __restrict__ chosen,
+                                                        uint64_t matchBase, uint32_t* __restrict__ slotsAll,
+                                                        uint4* __restrict__ state, const uint4* __restrict__ rec,
+                                                        int* __restrict__ status)
+{
+  __shared__ uint32_t fix[kWalkCap];
+  const Block B = blocks[blockIdx.x];
+  if (B.walkCount < 2) return;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  const uint32_t* L = chosen + (B.start - matchBase);
+  uint32_t T = state[B.walkFirst].z;  // true exit of sub-segment 0 (walked from the block start)
+  for (uint32_t k0 = 1; k0 < B.walkCount; k0 += 64) {
+    const uint32_t cnt = B.walkCount - k0 < 64u ? B.walkCount - k0 : 64u;
+    const uint32_t idxL = B.walkFirst + k0 + lane;
+    const uint4 r = lane < cnt ? rec[idxL] : make_uint4(0, 0, 0, 0);
+    uint32_t cur = 0;
+    while (cur < cnt) {
+      // lane j assumed entry r.w; its true entry is the exit of lane j - 1 (T for the first open lane)
+      uint32_t prevExit = __shfl_up(r.z, 1, 64);
+      if (lane == cur) prevExit = T;
+      const uint64_t bad = __ballot(lane >= cur && lane < cnt && r.w != prevExit);
+      const uint32_t js = bad ? (uint32_t)__builtin_ctzll(bad) : cnt;
+      if (lane >= cur && lane < js) {
+        // the assumption held: move the repaired matches in place (destination above the source)
+        uint32_t* slots = slotsAll + (uint64_t)idxL * (2 * kWalkCap);
+        for (uint32_t t = r.y; t-- > 0;) slots[r.x + t] = slots[t];
+        uint32_t* s32 = reinterpret_cast<uint32_t*>(state + idxL);
+        s32[0] = r.x;
+        s32[2] = r.z;
+      }
+      if (js == cnt) {
+        T = rdlane(r.z, cnt - 1u);
+        break;
+      }
+      // sub-segment k0 + js entered elsewhere: repaired again from its true entry
+      const uint32_t idx = B.walkFirst + k0 + js;
+      const uint32_t a = (k0 + js) * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+      uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
+      const WalkRepair W{L, slots, lane};
+      const uint4 st = state[idx];
+      const uint4 rr = W.run(fix, a, aNext, st, rdlane(prevExit, js), status);
+      __syncthreads();
+      for (uint32_t t = lane; t < rr.y; t += 64) slots[rr.x + t] = fix[t];
+      if (lane == 0) state[idx] = make_uint4(rr.x, st.y, rr.z, 0u);
+      __syncthreads();
+      T = rr.z;
+      cur = js + 1;
+    }
   }
 }
 
@@ -4394,6 +4555,8 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
   if (nsegs) hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB);
 }
 
+uint32_t dp_side_positions() { return kDpSide; }
+
 uint32_t find_lds_bytes() { return 65536 + 16; }
 uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 
@@ -4484,7 +4647,7 @@ uint32_t lazy_slots_per_walk() { return 2 * kLazyCap; }
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
                   uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, const uint32_t* longFlag, uint32_t* rmqUp,
-                  uint32_t* rmqDown, int* status, hipStream_t s)
+                  uint32_t* rmqDown, uint2* dpSide, uint4* dpRec, int* status, hipStream_t s)
 {
   (void)in;
   if (!nblocks) return;
@@ -4494,8 +4657,10 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
                      ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
   hipLaunchKernelGGL(k_dp_spec<true>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
                      ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
-  hipLaunchKernelGGL(k_dp_fix, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, mlen, mdist, matchBase, cost, sel, reach,
-                     segState, longFlag, rmqUp, rmqDown);
+  hipLaunchKernelGGL(k_dp_fix<true>, dim3(ndp), dim3(64), 0, s, blocks, dpSegs, ndp, mlen, mdist, matchBase, cost, sel,
+                     reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec);
+  hipLaunchKernelGGL(k_dp_fix<false>, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, ndp, mlen, mdist, matchBase, cost, sel,
+                     reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec);
 }
 
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
@@ -4507,10 +4672,16 @@ void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
   if (maxChain > 0 && nwalk) {
     hipLaunchKernelGGL(k_walk, dim3((nwalk + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs,
                        nwalk, chosen, matchBase, walkSlots, walkState, status);
-    hipLaunchKernelGGL(k_walk_fix, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState, status);
   }
-  // per-sub-segment scratch in posList (the parse's reach array, free by now)
+  // per-sub-segment scratch in posList (the parse's reach array, free by now): the repair records,
+  // then the token counts
   uint4* info = reinterpret_cast<uint4*>(posList);
+  if (maxChain > 0 && nwalk) {
+    hipLaunchKernelGGL(k_walk_fix_spec, dim3((nwalk + kWalkWaves - 1) / kWalkWaves), dim3(64 * kWalkWaves), 0, s, blocks,
+                       walkSegs, nwalk, chosen, matchBase, walkSlots, walkState, info, status);
+    hipLaunchKernelGGL(k_walk_fix_commit, dim3(nblocks), dim3(64), 0, s, blocks, chosen, matchBase, walkSlots, walkState, info,
+                       status);
+  }
   uint2* blockTail = reinterpret_cast<uint2*>(info + nwalk);
   const uint32_t segGrid = (nwalk + kSegWaves - 1) / kSegWaves;
   if (maxChain > 0 && nwalk) {
