@@ -193,7 +193,9 @@ def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
 def pmc_traffic(cfg):
     """HBM bytes per k_find_sorted launch from the newest profiles/*_pmc.json of this workload."""
     best = None
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))):
+    # tags run r02a..r02z, r02aa..r02az: order by tag length first so r02av sorts after r02o
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))
+    for path in sorted(paths, key=lambda p: (len(os.path.basename(p)), os.path.basename(p))):
         try:
             with open(path) as f:
                 rec = json.load(f)
