@@ -62,6 +62,14 @@ struct Window {
 
 constexpr uint64_t kWaitLimit = 100000000ull * 60;  // 60 s of s_memrealtime (100 MHz)
 
+// The LDS ring holds the last kRing output bytes (16 KiB: ten 64-lane workgroups per CU instead of two
+// with the reference's full 64 KiB history).  Bytes further back are read from `out` itself: the wave
+// drains its stores (s_waitcnt vmcnt(0) + workgroup acquire) whenever it has written kSync bytes since
+// the last drain, so every byte below the ring's reach has been written and is visible to all lanes
+// (kSync <= kRing - 64: a read below cur + 64 - kRing is then below the drained position).
+constexpr uint32_t kRing = 16384;
+constexpr uint32_t kSync = kRing / 2;
+
 // v_writelane (the LLVM intrinsic by name): lane `l` of v becomes the uniform `x`
 extern "C" __device__ int sz4_un_writelane(int, int, int) __asm("llvm.amdgcn.writelane.i32");
 __device__ __forceinline__ uint32_t un_wrlane(uint32_t v, uint32_t x, uint32_t l)
@@ -111,42 +119,126 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
     if ((ns & 63u) == 0u) seq[ns - 64u + lane] = buf;
   };
   Window win{f, n, 0, 0};
-  win.fill(r, lane);
-  while (r < end) {
-    if (ns >= cap) return kNone;  // cannot happen in a well-formed block
+  // One sequence byte by byte through the window (smallz4cat.c:212-323): 0 next, 1 block done, 2 malformed.
+  // Taken for what the pre-decoded headers below do not cover: extended literal runs, match lengths
+  // with more than one extension byte, headers reaching past the register window.
+  auto one_seq = [&]() -> int {
     const uint32_t tok = win.byte(r++, lane);
     uint64_t lits = tok >> 4;
     if (lits == 15) {
       uint32_t x;
       do {
-        if (r >= end) return kNone;
+        if (r >= end) return 2;
         x = win.byte(r++, lane);
         lits += x;
       } while (x == 255);
     }
-    if (r + lits > end) return kNone;
+    if (r + lits > end) return 2;
     const uint32_t frel = (uint32_t)(r - B.src);
     w += lits;
     r += lits;
     if (r == end) {  // the last sequence has literals only
       push((uint32_t)lits, 0u, 0u, frel);
-      break;
+      return 1;
     }
-    if (r + 2 > end) return kNone;
+    if (r + 2 > end) return 2;
     const uint32_t off = win.byte(r, lane) | (win.byte(r + 1, lane) << 8);
     r += 2;
-    if (off == 0) return kNone;  // "invalid offset" (smallz4cat.c:265-267)
+    if (off == 0) return 2;  // "invalid offset" (smallz4cat.c:265-267)
     uint64_t ml = kMinMatch + (tok & 15);
     if (ml == kMinMatch + 15) {
       uint32_t x;
       do {
-        if (r >= end) return kNone;
+        if (r >= end) return 2;
         x = win.byte(r++, lane);
         ml += x;
       } while (x == 255);
     }
     push((uint32_t)lits, (uint32_t)ml, off, frel);
     w += ml;
+    return 0;
+  };
+  while (r < end) {
+    // Pre-decode a header at every window position q = 4 lane + k: token | offset << 8 | first match
+    // extension byte << 24, or ~0 when the header needs the byte-wise path (literal run >= 15, or its
+    // offset / extension byte past the window).  The walk then costs one readlane per sequence.
+    win.fill(r, lane);
+    uint32_t cand[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t tok = (win.w >> (8 * k)) & 0xFFu;
+      const uint32_t a = 4u * lane + (uint32_t)k + 1u + (tok >> 4);  // window index of the offset
+      const uint32_t ia = (a >> 2) << 2;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)ia, (int)win.w);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ia + 4u), (int)win.w);
+      const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (a & 3u)));
+      const uint32_t last = a + 1u + ((tok & 15u) == 15u ? 1u : 0u);  // last window byte the header reads
+      const bool ok = (tok >> 4) != 15u && last < 256u;
+      cand[k] = ok ? (tok | (v << 8)) : 0xFFFFFFFFu;  // v's bytes 0-2: offset, extension byte
+    }
+    int st = -1;  // -1: refill, 0: byte-wise sequence, 1: done
+    for (;;) {
+      if (r >= end) { st = 1; break; }
+      if (ns >= cap) return kNone;  // cannot happen in a well-formed block
+      const uint32_t q = (uint32_t)(r - win.base);
+      if (q >= 192u) break;
+      const uint32_t ql = q >> 2;
+      const uint32_t c0 = un_rdlane(cand[0], ql), c1 = un_rdlane(cand[1], ql);
+      const uint32_t c2 = un_rdlane(cand[2], ql), c3 = un_rdlane(cand[3], ql);
+      const uint32_t pk = (q & 2u) ? ((q & 1u) ? c3 : c2) : ((q & 1u) ? c1 : c0);
+      if (pk == 0xFFFFFFFFu) {
+        if (q >= 64u) break;  // refill at r first: the header may fit the next window
+        st = 0;
+        break;
+      }
+      const uint32_t tok = pk & 0xFFu;
+      const uint64_t lits = tok >> 4;
+      const uint64_t r1 = r + 1;
+      if (r1 + lits > end) return kNone;
+      const uint32_t frel = (uint32_t)(r1 - B.src);
+      w += lits;
+      const uint64_t r2 = r1 + lits;
+      if (r2 == end) {
+        push((uint32_t)lits, 0u, 0u, frel);
+        r = r2;
+        st = 1;
+        break;
+      }
+      if (r2 + 2 > end) return kNone;
+      const uint32_t off = (pk >> 8) & 0xFFFFu;
+      if (off == 0) return kNone;
+      uint64_t rn = r2 + 2;
+      uint64_t ml = kMinMatch + (tok & 15u);
+      bool more = false;
+      if ((tok & 15u) == 15u) {
+        if (rn >= end) return kNone;
+        const uint32_t x = pk >> 24;
+        rn++;
+        ml += x;
+        more = x == 255u;
+      }
+      r = rn;
+      if (more) {  // further extension bytes, byte-wise (a refill makes the headers stale)
+        uint32_t x;
+        do {
+          if (r >= end) return kNone;
+          x = win.byte(r++, lane);
+          ml += x;
+        } while (x == 255);
+        push((uint32_t)lits, (uint32_t)ml, off, frel);
+        w += ml;
+        break;
+      }
+      push((uint32_t)lits, (uint32_t)ml, off, frel);
+      w += ml;
+    }
+    if (st == 1) break;
+    if (st == 0) {
+      if (ns >= cap) return kNone;
+      const int e = one_seq();
+      if (e == 2) return kNone;
+      if (e == 1) break;
+    }
   }
   if (ns & 63u) {
     const uint32_t b = ns & ~63u;
@@ -170,6 +262,7 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
   uint64_t floorPos = B.dst;  // output below this is read only after its blocks are done
   uint32_t waitIdx = bi;
   uint64_t w = 0;             // bytes decoded so far
+  uint64_t synced = B.dst;    // this block's output below it is drained and readable from `out`
   for (uint32_t b0 = 0; b0 < B.nseq; b0 += 64) {
     const uint32_t cnt = B.nseq - b0 < 64u ? B.nseq - b0 : 64u;
     const uint4 q = lane < cnt ? seq[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
@@ -211,13 +304,13 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
           const uint8_t v = (uint8_t)(((rel & 4u) ? c : a) >> (8 * (rel & 3u)));
           if (lane < L) {
             out[P + lane] = v;
-            ring[(P + lane) & 0xFFFFu] = v;
+            ring[(P + lane) & (kRing - 1u)] = v;
           }
         } else {
           for (uint64_t k = lane; k < L; k += 64) {
             const uint8_t v = f[B.src + fr + k];
             out[P + k] = v;
-            ring[(P + k) & 0xFFFFu] = v;
+            ring[(P + k) & (kRing - 1u)] = v;
           }
         }
       }
@@ -249,18 +342,26 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
         // 64 KiB even for matches longer than that.
         const uint32_t qq = off >= 64u ? off : off * ((64u + off - 1u) / off);
         for (uint64_t k = 0; k < M; k += 64) {
+          const uint64_t cur = Q + k;  // every output byte below it has been stored
+          if (cur - synced >= kSync) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            synced = cur;
+          }
+          // ring slots of this step's reads are still intact above cur + 64 - kRing
+          const int64_t ringLo = (int64_t)cur + 64 - (int64_t)kRing;
           const uint64_t jj = k + lane;
           const int64_t s = k == 0 ? lo + (int64_t)(off >= 64u ? lane : lane % off) : (int64_t)(Q + jj) - (int64_t)qq;
           uint8_t v = 0;
           if (jj < M) {
-            if (s >= (int64_t)B.dst) v = ring[(uint64_t)s & 0xFFFFu];
-            else if (s >= 0) v = out[s];                                   // an earlier block (finished)
+            if (s >= (int64_t)B.dst && s >= ringLo) v = ring[(uint64_t)s & (kRing - 1u)];
+            else if (s >= 0) v = out[s];  // drained output of this block, or an earlier (finished) block
             else if ((uint64_t)(-s) <= dl) v = dict[dl - (uint64_t)(-s)];  // the dictionary's tail
             // else 0: before the history (oz_unlz4's zero-initialised history)
           }
           if (jj < M) {
             out[Q + jj] = v;
-            ring[(Q + jj) & 0xFFFFu] = v;
+            ring[(Q + jj) & (kRing - 1u)] = v;
           }
         }
       }
@@ -353,7 +454,7 @@ __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__
                                                      uint32_t nb, const uint4* __restrict__ seqAll, uint8_t* __restrict__ out,
                                                      const uint8_t* __restrict__ dict, uint64_t dl, uint32_t* __restrict__ flags)
 {
-  __shared__ uint8_t ring[65536];
+  __shared__ uint8_t ring[kRing];
   const uint32_t lane = threadIdx.x;
   uint32_t* done = flags;
   uint32_t* status = flags + nb;
