@@ -158,10 +158,14 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
     w += ml;
     return 0;
   };
+  // A sequence starting 20 or more bytes before the block end passes every bounds check of one_seq
+  // (its header reads at most 18 bytes past the token, its literals end before the block does), so the
+  // walk below checks nothing but a zero offset and runs on block-relative 32-bit cursors.
+  const uint32_t fastEnd = B.len > 20u ? B.len - 20u : 0u;
   while (r < end) {
-    // Pre-decode a header at every window position q = 4 lane + k: token | offset << 8 | first match
-    // extension byte << 24, or ~0 when the header needs the byte-wise path (literal run >= 15, or its
-    // offset / extension byte past the window).  The walk then costs one readlane per sequence.
+    // Pre-decode a header at every window position q = 4 lane + k: token | offset << 8 | extension
+    // byte << 24, or ~0 when the header needs the byte-wise path (literal run >= 15, a second match
+    // extension byte, or bytes past the register window).  The walk costs one readlane per sequence.
     win.fill(r, lane);
     uint32_t cand[4];
 #pragma unroll
@@ -172,73 +176,41 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
       const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)ia, (int)win.w);
       const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ia + 4u), (int)win.w);
       const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (a & 3u)));
-      const uint32_t last = a + 1u + ((tok & 15u) == 15u ? 1u : 0u);  // last window byte the header reads
-      const bool ok = (tok >> 4) != 15u && last < 256u;
+      const bool ext = (tok & 15u) == 15u;
+      const uint32_t last = a + 1u + (ext ? 1u : 0u);  // last window byte the header reads
+      const bool ok = (tok >> 4) != 15u && last < 256u && !(ext && ((v >> 16) & 0xFFu) == 255u);
       cand[k] = ok ? (tok | (v << 8)) : 0xFFFFFFFFu;  // v's bytes 0-2: offset, extension byte
     }
-    int st = -1;  // -1: refill, 0: byte-wise sequence, 1: done
-    for (;;) {
-      if (r >= end) { st = 1; break; }
-      if (ns >= cap) return kNone;  // cannot happen in a well-formed block
-      const uint32_t q = (uint32_t)(r - win.base);
+    const uint32_t wb = (uint32_t)(win.base - B.src);  // window base, block-relative (r >= B.src >= base - 3)
+    uint32_t rr = (uint32_t)(r - B.src);
+    bool slow = false;
+    while (rr < fastEnd) {
+      const uint32_t q = rr - wb;
       if (q >= 192u) break;
       const uint32_t ql = q >> 2;
       const uint32_t c0 = un_rdlane(cand[0], ql), c1 = un_rdlane(cand[1], ql);
       const uint32_t c2 = un_rdlane(cand[2], ql), c3 = un_rdlane(cand[3], ql);
       const uint32_t pk = (q & 2u) ? ((q & 1u) ? c3 : c2) : ((q & 1u) ? c1 : c0);
       if (pk == 0xFFFFFFFFu) {
-        if (q >= 64u) break;  // refill at r first: the header may fit the next window
-        st = 0;
+        slow = q < 64u;  // else refill at rr first: the header may fit the next window
         break;
       }
-      const uint32_t tok = pk & 0xFFu;
-      const uint64_t lits = tok >> 4;
-      const uint64_t r1 = r + 1;
-      if (r1 + lits > end) return kNone;
-      const uint32_t frel = (uint32_t)(r1 - B.src);
-      w += lits;
-      const uint64_t r2 = r1 + lits;
-      if (r2 == end) {
-        push((uint32_t)lits, 0u, 0u, frel);
-        r = r2;
-        st = 1;
-        break;
-      }
-      if (r2 + 2 > end) return kNone;
       const uint32_t off = (pk >> 8) & 0xFFFFu;
-      if (off == 0) return kNone;
-      uint64_t rn = r2 + 2;
-      uint64_t ml = kMinMatch + (tok & 15u);
-      bool more = false;
-      if ((tok & 15u) == 15u) {
-        if (rn >= end) return kNone;
-        const uint32_t x = pk >> 24;
-        rn++;
-        ml += x;
-        more = x == 255u;
-      }
-      r = rn;
-      if (more) {  // further extension bytes, byte-wise (a refill makes the headers stale)
-        uint32_t x;
-        do {
-          if (r >= end) return kNone;
-          x = win.byte(r++, lane);
-          ml += x;
-        } while (x == 255);
-        push((uint32_t)lits, (uint32_t)ml, off, frel);
-        w += ml;
-        break;
-      }
-      push((uint32_t)lits, (uint32_t)ml, off, frel);
-      w += ml;
+      if (off == 0) return kNone;  // "invalid offset" (smallz4cat.c:265-267)
+      const uint32_t lits = (pk >> 4) & 15u, nib = pk & 15u;
+      const uint32_t ml = kMinMatch + nib + (nib == 15u ? pk >> 24 : 0u);
+      push(lits, ml, off, rr + 1u);
+      w += lits + ml;
+      rr += 3u + lits + (nib == 15u ? 1u : 0u);
     }
-    if (st == 1) break;
-    if (st == 0) {
-      if (ns >= cap) return kNone;
-      const int e = one_seq();
-      if (e == 2) return kNone;
-      if (e == 1) break;
-    }
+    r = B.src + rr;
+    if (rr < fastEnd && !slow) continue;  // refill
+    // byte-wise: a header the window could not pre-decode, or the block's last 20 bytes
+    if (r >= end) break;
+    if (ns >= cap) return kNone;  // cannot happen in a well-formed block
+    const int e = one_seq();
+    if (e == 2) return kNone;
+    if (e == 1) break;
   }
   if (ns & 63u) {
     const uint32_t b = ns & ~63u;
