@@ -3356,6 +3356,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   uint32_t nextL = segHi - (int32_t)lane >= segLo ? L[segHi - lane] : 0u;
   auto key_cost = [&](int32_t, uint32_t key) -> uint32_t { return key >> 8; };
   RunEnd chain;
+  bool noMatch = true;  // no position of the segment has a match: k_dp_fix repairs it in closed form
 
   for (int32_t hi = segHi; hi >= segLo; hi -= 64) {
     const int32_t lo = hi - 63 > segLo ? hi - 63 : segLo;
@@ -3367,7 +3368,9 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
     // per position hi - t in lane t: its best key (0 = slow path, see bestBuf), its cost, its choice
     uint32_t kvBuf = 0xFFFFFFFFu, mcBuf = 0, bestBuf = 1;
     const uint32_t cnt = (uint32_t)(hi - lo + 1);
-    if (__ballot(lane < cnt && myL >= (uint32_t)kMinMatch) == 0) {
+    const bool litChunk = __ballot(lane < cnt && myL >= (uint32_t)kMinMatch) == 0;
+    noMatch = noMatch && litChunk;
+    if (litChunk) {
       // no match anywhere in the chunk: every position is a literal, costs in closed form
       const uint32_t t = lane, run = lits + t + 1u;
       const uint32_t nb = run >= litBump ? 1u + (run - litBump) / 255u : 0u;
@@ -3631,7 +3634,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
       }
     }
   }
-  if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, 0u, 0u);
+  if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, noMatch ? 1u : 0u, 0u);
 }
 
 // k_dp_fix<true>: the repair of every segment k >= 1 of a block without range minima at once, each from
@@ -3678,6 +3681,14 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   const Block B = blocks[bIdx];
   if (B.dpCount <= 1) return;
   const uint32_t lane = threadIdx.x;
+  if constexpr (kPar) {
+    // a segment without any match cannot converge (that needs a match): nothing written, k_dp_fix<false>
+    // repairs it in closed form
+    if (segState[blockIdx.x].z != 0u) {
+      if (lane == 0) dpRec[blockIdx.x] = make_uint4(dpSegs[blockIdx.x].hi + 1u, 0u, 0u, 0u);
+      return;
+    }
+  }
   const uint64_t base = B.start - matchBase;
   const uint32_t* L = mlen + base;
   const uint16_t* D = mdist + base;
@@ -3741,15 +3752,22 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       }
       // repaired from a wrong state: the speculative values back, then the serial repair
       uint2* sd = side + (uint64_t)(B.dpFirst + k) * kDpSide;
-      for (uint32_t t2 = lane; t2 <= (uint32_t)hi - rConv; t2 += 64) {
+      for (int32_t t2 = (int32_t)lane; hi - t2 >= (int32_t)rConv; t2 += 64) {  // rConv = hi + 1: nothing written
         const uint2 v = sd[t2];
-        cost[hi - (int32_t)t2] = v.x;
-        S[hi - (int32_t)t2] = v.y;
+        cost[hi - t2] = v.x;
+        S[hi - t2] = v.y;
       }
-      __threadfence();  // the stores are complete and the L1 is invalidated before the reloads below
+      // the stores complete before the reloads below; only this wavefront reads them (same CU), so a
+      // workgroup-scope fence does -- __threadfence() would write back and invalidate the XCD's whole L2
+      // (buffer_wbl2 sc1 + buffer_inv sc1 on gfx950) once per restored segment
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
     }
     const uint4 st = segState[B.dpFirst + k - 1];  // exact state below the segment above
     uint32_t lits = st.x, litBump = st.y;
+    // no match in the segment (k_dp_spec): every chunk is closed-form literals and none converges, so
+    // nothing needs loading (this segment's own state record is overwritten only at its end)
+    const bool noMatch = !kPar && segState[B.dpFirst + k].z != 0u;
     uint32_t costNext = exact_above((uint32_t)hi + 1);
     uint32_t cbuf = exact_above((uint32_t)hi + 1 + ((lane - (uint32_t)hi - 1u) & 63u));
     // exact cost of j > i: this pass's own results (ring / HBM) inside the segment, above it the table
@@ -3788,7 +3806,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       nC = in ? cost[ip] : 0u;
       nR = in ? R[ip] : 0u;
     };
-    load_chunk(hi);
+    nL = nD = nS = nC = nR = 0u;
+    if (!noMatch) load_chunk(hi);
     for (int32_t h = hi; h >= lo && !done; h -= 64) {
       const int32_t ip = h - (int32_t)lane;
       const bool in = ip >= lo;
@@ -3799,7 +3818,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       asm volatile("v_mov_b32 %0, %1" : "=v"(cS) : "v"(nS));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cC) : "v"(nC));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cR) : "v"(nR));
-      if (h - 64 >= lo) load_chunk(h - 64);
+      if (h - 64 >= lo && !noMatch) load_chunk(h - 64);
       const int32_t cl = h - 63 > lo ? h - 63 : lo;
       const uint32_t cnt = (uint32_t)(h - cl + 1);
       if constexpr (kPar) {
@@ -3807,7 +3826,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         if (in) side[(uint64_t)blockIdx.x * kDpSide + (uint32_t)(hi - ip)] = make_uint2(cC, cS);
         lowW = cl;
       }
-      if (__ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
+      if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
         auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
           const uint32_t run = lits + t + 1u;
@@ -3825,12 +3844,14 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         const uint32_t tl = ((uint32_t)h - lane) & 63u;
         if (tl < cnt) cbuf = lit_cost(tl, nb2);
         chain.valid = chain.pending = false;
-        const uint32_t delta = cT - cC;
-        uint32_t dPrev = __shfl_up(delta, 1, 64);
-        if (lane == 0) dPrev = prevDelta;
-        const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
-        if (chg) runTop = h - (63 - (int32_t)__builtin_clzll(chg));
-        prevDelta = rdlane(delta, cnt - 1u);
+        if (!noMatch) {  // convergence bookkeeping (a segment without matches never converges)
+          const uint32_t delta = cT - cC;
+          uint32_t dPrev = __shfl_up(delta, 1, 64);
+          if (lane == 0) dPrev = prevDelta;
+          const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
+          if (chg) runTop = h - (63 - (int32_t)__builtin_clzll(chg));
+          prevDelta = rdlane(delta, cnt - 1u);
+        }
         lits += cnt;
         litBump += 255u * rdlane(nb, cnt - 1u);
         costNext = rdlane(cT, cnt - 1u);
