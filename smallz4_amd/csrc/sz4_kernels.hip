@@ -3289,7 +3289,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __r
 constexpr int kSpecWaves = 4;  // independent segments per workgroup (workgroup slots, not LDS, bound occupancy)
 
 template <bool kRmq>
-__global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __restrict__ blocks,
+__device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
                                                              const DpSeg* __restrict__ dpSegs, uint32_t ndp,
                                                              const uint32_t* __restrict__ mlen,
                                                              const uint16_t* __restrict__ mdist, uint64_t matchBase,
@@ -3637,6 +3637,25 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec(const Block* __rest
   if (lane == 0) segState[segIdx] = make_uint4(lits, litBump, noMatch ? 1u : 0u, 0u);
 }
 
+// The lean parse at <= 80 SGPRs: a wave takes ceil(sgpr / 16) * 16 + 16 of the SIMD's 800, so its natural
+// 99 admit 6 waves per SIMD and 80 admit 8 (23 SGPRs spill to VGPR lanes).  The range-minimum variant
+// would spill 133 and keeps its registers.
+#define SZ4_DP_SPEC_ARGS                                                                                   \
+  const Block *__restrict__ blocks, const DpSeg *__restrict__ dpSegs, uint32_t ndp,                        \
+      const uint32_t *__restrict__ mlen, const uint16_t *__restrict__ mdist, uint64_t matchBase,           \
+      uint32_t *__restrict__ costAll, uint32_t *__restrict__ sel, uint32_t *__restrict__ reach,            \
+      uint4 *__restrict__ segState, const uint32_t *__restrict__ longFlag, uint32_t *__restrict__ upAll,   \
+      uint32_t *__restrict__ downAll
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(80))) void k_dp_spec_lean(SZ4_DP_SPEC_ARGS)
+{
+  dp_spec_body<false>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
+}
+__global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
+{
+  dp_spec_body<true>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
+}
+#undef SZ4_DP_SPEC_ARGS
+
 // k_dp_fix<true>: the repair of every segment k >= 1 of a block without range minima at once, each from
 // the SPECULATIVE costs and state of segment k - 1 (one wavefront per segment).  Choices depend on cost
 // differences only, so the result is exact whenever everything it read lies in the part of k - 1 that
@@ -3685,7 +3704,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     // a segment without any match cannot converge (that needs a match): nothing written, k_dp_fix<false>
     // repairs it in closed form
     if (segState[blockIdx.x].z != 0u) {
-      if (lane == 0) dpRec[blockIdx.x] = make_uint4(dpSegs[blockIdx.x].hi + 1u, 0u, 0u, 0u);
+      if (lane == 0) dpRec[blockIdx.x] = make_uint4(dpSegs[blockIdx.x].hi + 1u, 0u, 0u, 2u);
       return;
     }
   }
@@ -3724,6 +3743,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   uint4 recV = make_uint4(0u, 0u, 0u, 0u);
   uint32_t prevV = 0, prevConv = 0;  // offset below segment k - 1's convergence point, that point
   bool prevDone = true;              // segment k - 1's repair converged (segment 0 is exact)
+  bool recNoMatch = false;           // k_dp_fix<true>'s record: the segment has no match (flag 2)
 
   for (uint32_t k = kFirst; k < kEnd; k++) {
     const DpSeg G = dpSegs[B.dpFirst + k];
@@ -3736,6 +3756,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       const uint32_t t = (k - 1u) & 63u;
       const uint32_t rConv = rdlane(recV.x, t), rDelta = rdlane(recV.y, t);
       const uint32_t rReach = rdlane(recV.z, t), rFlag = rdlane(recV.w, t);
+      recNoMatch = (rFlag & 2u) != 0u;
       if ((rFlag & 1u) && (k == 1u || (prevDone && rReach < prevConv))) {
         // everything it read was exact - prevV: its costs are exact - prevV
         if (lane == 0) {
@@ -3767,7 +3788,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     uint32_t lits = st.x, litBump = st.y;
     // no match in the segment (k_dp_spec): every chunk is closed-form literals and none converges, so
     // nothing needs loading (this segment's own state record is overwritten only at its end)
-    const bool noMatch = !kPar && segState[B.dpFirst + k].z != 0u;
+    // (blocks k_dp_fix<true> ran over carry the flag in their records, already in registers)
+    const bool noMatch = !kPar && (par ? recNoMatch : segState[B.dpFirst + k].z != 0u);
     uint32_t costNext = exact_above((uint32_t)hi + 1);
     uint32_t cbuf = exact_above((uint32_t)hi + 1 + ((lane - (uint32_t)hi - 1u) & 63u));
     // exact cost of j > i: this pass's own results (ring / HBM) inside the segment, above it the table
@@ -4674,9 +4696,9 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
   if (!nblocks) return;
   if (maxChain <= (uint32_t)kGreedyMax || !ndp) return;
   // every segment is parsed by exactly one of the two instantiations (by its block's longFlag)
-  hipLaunchKernelGGL(k_dp_spec<false>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
+  hipLaunchKernelGGL(k_dp_spec_lean, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
                      ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
-  hipLaunchKernelGGL(k_dp_spec<true>, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
+  hipLaunchKernelGGL(k_dp_spec_rmq, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
                      ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
   hipLaunchKernelGGL(k_dp_fix<true>, dim3(ndp), dim3(64), 0, s, blocks, dpSegs, ndp, mlen, mdist, matchBase, cost, sel,
                      reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec);
