@@ -1725,7 +1725,7 @@ __device__ __forceinline__ uint32_t wave_exact_prefix(const Src& src, uint64_t p
 }
 
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                              const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                              const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                              uint2* __restrict__ skipAll, const uint32_t* __restrict__ rankAll,
@@ -2102,6 +2102,28 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9(const uint8_t* __re
     }
   }
 }
+
+// k_find_long9_lds (the whole window in LDS, 64 KiB + 16 B) at <= 80 SGPRs: two 16-wave workgroups per
+// CU (8 waves per SIMD) instead of one at 106; <false> stages up to 128 KiB and runs alone on its CU anyway.
+#define SZ4_LONG9_ARGS                                                                                        \
+  const uint8_t *__restrict__ in, const Segment *__restrict__ segs, const Block *__restrict__ blocks,         \
+      const Interval *__restrict__ ivAll, const uint32_t *__restrict__ ivCount,                               \
+      const uint2 *__restrict__ compactAll, uint2 *__restrict__ skipAll, const uint32_t *__restrict__ rankAll, \
+      const uint32_t *__restrict__ longBits, const uint32_t *__restrict__ segLong, uint32_t *__restrict__ mlen, \
+      uint16_t *__restrict__ mdist, uint64_t matchBase, uint32_t *__restrict__ longFlag,                      \
+      uint32_t *__restrict__ specLen, uint32_t *__restrict__ specDist, int fixMode
+#define SZ4_LONG9_PASS in, segs, blocks, ivAll, ivCount, compactAll, skipAll, rankAll, longBits, segLong, mlen, mdist, \
+                       matchBase, longFlag, specLen, specDist, fixMode
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(80))) void k_find_long9_lds(SZ4_LONG9_ARGS)
+{
+  find_long9_body<true>(SZ4_LONG9_PASS);
+}
+__global__ __launch_bounds__(kFindThreads) void k_find_long9_hbm(SZ4_LONG9_ARGS)
+{
+  find_long9_body<false>(SZ4_LONG9_PASS);
+}
+#undef SZ4_LONG9_ARGS
+#undef SZ4_LONG9_PASS
 
 // ================================================================================================
 // k_find_big (-9, between pass 1 and pass 2): the targets pass 1 handed on because their key group
@@ -4617,7 +4639,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     // dynamic-LDS limits are per function and device: set them on every launch (a host-side call,
     // no synchronisation) rather than caching them process-wide
     const void* fn = pass == 1 ? (const void*)k_find_sorted_lds
-                     : unlimited ? (const void*)k_find_long9<true> : (const void*)k_find<true>;
+                     : unlimited ? (const void*)k_find_long9_lds : (const void*)k_find<true>;
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
@@ -4631,7 +4653,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
           hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
                              compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
       for (int fix = 0; fix < 2; fix++)
-        hipLaunchKernelGGL(k_find_long9<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
+        hipLaunchKernelGGL(k_find_long9_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
                            specDist, fix);
     } else
@@ -4651,9 +4673,9 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount,
                              compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
-      hipFuncSetAttribute((const void*)k_find_long9<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+      hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
-        hipLaunchKernelGGL(k_find_long9<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+        hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
                            compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen, specDist,
                            fix);
     }
