@@ -96,6 +96,12 @@ class Compressor:
             except BaseException as e:  # noqa: BLE001 -- re-raised after the call
                 err.append(e)
                 return 0
+            if b is None:
+                return 0
+            if len(b) > n:
+                # the native buffer holds n bytes: more is a caller error, not a silent overrun
+                err.append(ValueError(f"read({n}) returned {len(b)} bytes"))
+                return 0
             if b:
                 ctypes.memmove(data, b, len(b))
             return len(b)

@@ -690,7 +690,9 @@ constexpr uint32_t kSatQ = 128;  // saturated-candidate queue per wavefront (flu
 template <bool kLds>
 constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
-constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_long9
+constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_big / k_find_long9
+constexpr uint32_t kBigRun = 256;     // the same for a run key (vvvv) in blocks k_find_big takes
+__device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
 constexpr uint32_t kFlagRmq = 1;   // longFlag: the block has matches of kRmqLen+ (other than same-letter runs)
 constexpr uint32_t kFlagRun = 2;   // longFlag: a distance-1 match longer than MaxSameLetter (bounded chains)
@@ -836,7 +838,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
     // -9, a target with more than kBigGroup candidates (runs, periodic data): left to k_find_long9,
     // which walks in text order and prunes with the previous target's result
-    const bool big = unlimited && cut == kNone && active && slot - gs > kBigGroup;
+    // (k_find_big takes blocks without a lookback cut or shortcut intervals; there run keys go from kBigRun on)
+    const bool lpfRun = B.cut == kNone && ivCount[S.block] == 0u && (B.prev == kNoBlock || ivCount[B.prev] == 0u);
+    const bool big = unlimited && cut == kNone && active && slot - gs > (lpfRun && run_key(me0) ? kBigRun : kBigGroup);
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
@@ -2147,8 +2151,35 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9_hbm(SZ4_LONG9_ARGS)
 // Only blocks without a lookback cut or shortcut intervals (independent blocks): the identity needs
 // every candidate position to be a chain position.
 // ================================================================================================
-constexpr uint32_t kMaxBigGroups = 16;  // > 128 Ki window slots / kBigGroup
+constexpr uint32_t kMaxBigGroups = 32;  // > 128 Ki window slots / kBigGroup, plus run-key groups
 constexpr uint32_t kClsNone = 256;      // preceding byte class of a position without a chain predecessor
+// run-key groups (key vvvv, runs of one byte value) are binned by their run length R (bytes equal to v
+// from the position on, within the block): a candidate of the same R shares R bytes and the next one
+// decides; every other R gives min(R(p), R(c))
+constexpr uint32_t kRunCap = 256;                             // R = 4..255 exact, 256 = at least 256
+constexpr uint32_t kBinRun0 = kClsNone + 1;                   // bins 0..256: class of a non-run member
+constexpr uint32_t kBins = kBinRun0 + 2 * (kRunCap - 3);      // then per R: run interior, run start
+constexpr uint32_t kNoBin = 0xFFFFFFFFu;
+static_assert(kBins <= kFindThreads, "one bin per thread in the bin scan");
+
+
+// exclusive prefix sums of v over the workgroup's threads (thread i: bin i); total in *tot
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* tot)
+{
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t incl = wave_incl_scan_add(v);
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (uint32_t w = 0; w < kFindThreads / 64; w++) {
+    const uint32_t x = wsum[w];
+    base += w < wave ? x : 0u;
+    all += x;
+  }
+  __syncthreads();
+  if (tot) *tot = all;
+  return base + incl - v;
+}
 
 template <bool kLds>
 __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
@@ -2163,9 +2194,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_groups[2 * kMaxBigGroups];
   __shared__ uint32_t s_ng, s_next;
-  __shared__ uint32_t s_cls[kClsNone + 2], s_tcls[kClsNone + 2];  // class starts (candidates, targets)
-  __shared__ uint32_t s_cur[2][kClsNone + 1];                      // scatter cursors
-  __shared__ uint32_t s_chunk[kClsNone + 2];                       // first chunk of each class
+  __shared__ uint32_t s_cls[kBins + 1], s_tcls[kBins + 1];  // bin starts (candidates, targets)
+  __shared__ uint32_t s_cur[2][kBins];                      // counts, then scatter cursors
+  __shared__ uint32_t s_wsum[kFindThreads / 64];
   __shared__ uint32_t s_hasHead[kFindThreads / 64], s_outValid[kFindThreads / 64];
   __shared__ uint64_t s_outKey[kFindThreads / 64];
   const Segment S = segs[blockIdx.x];
@@ -2178,12 +2209,14 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   const uint32_t E = (uint32_t)(S.s1 - S.w0);  // no intervals: every window position is a slot
   const bool small = compact_small(S);
 
-  // 1. big groups: last slot s of a group with s - gs > kBigGroup
+  // 1. big groups: the last slot s of a group holding a target that pass 1 handed on (more than
+  //    kBigGroup candidates, or kBigRun for a run key: the same predicate as k_find_sorted's)
   if (tid == 0) s_ng = 0;
   __syncthreads();
   for (uint32_t s = tid; s < E; s += kFindThreads) {
     const uint32_t g = slot_gs(compact, small, E, s);
-    if (s - g > kBigGroup && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g)) {
+    if (s - g > kBigRun && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g) &&
+        (s - g > kBigGroup || run_key(gload4(in, S.w0 + slot_pos(compact, small, s))))) {
       const uint32_t k = atomicAdd(&s_ng, 1u);
       if (k < kMaxBigGroups) {
         s_groups[2 * k] = g;
@@ -2214,39 +2247,60 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
   auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
-  uint32_t* C = reinterpret_cast<uint32_t*>(scratchAll + S.elemOff);  // candidates: cls << 17 | rel
-  uint32_t* T = C + E;                                                 // targets: rel
+  // bin of a member: its class, or for a run key its run length R (capped at kRunCap, within the block)
+  // and whether it starts the run (its class is not the run's byte)
+  auto bin_of = [&](uint64_t q, uint32_t key) -> uint32_t {
+    const uint32_t c = cls_of(q);
+    if (!run_key(key)) return c;
+    const uint64_t left = B.end - q;
+    const uint32_t lim = left < kRunCap ? (uint32_t)left : kRunCap;
+    uint32_t r = 4;
+    while (r < lim) {
+      const uint32_t x = src.ld4(q + r) ^ key;
+      if (x) {
+        r += (uint32_t)__builtin_ctz(x) >> 3;
+        break;
+      }
+      r += 4;
+    }
+    r = r < lim ? r : lim;
+    return kBinRun0 + 2u * (r - 4u) + (c != (key & 0xFFu) ? 1u : 0u);
+  };
+  auto is_target = [&](uint32_t s, uint32_t ga, uint64_t q, uint32_t key) {
+    return q >= S.s0 && s - ga > (run_key(key) ? kBigRun : kBigGroup);
+  };
+  uint32_t* C = reinterpret_cast<uint32_t*>(scratchAll + S.elemOff);  // candidates: bin << 17 | rel
+  uint32_t* T = C + E;                                                 // targets: bin << 17 | rel
   __syncthreads();
 
   for (uint32_t gi = 0; gi < ng; gi++) {
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
-    for (uint32_t k = tid; k < 2 * (kClsNone + 1); k += kFindThreads) (&s_cur[0][0])[k] = 0;
+    for (uint32_t k = tid; k < 2 * kBins; k += kFindThreads) (&s_cur[0][0])[k] = 0;
     __syncthreads();
-    // counts per class (candidates: the whole group; targets: pass 1's big ones)
+    // counts per bin (candidates: the whole group; targets: pass 1's big ones)
     for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
       const uint32_t r = slot_pos(compact, small, s);
       const uint64_t q = S.w0 + r;
-      const uint32_t c = cls_of(q);
-      atomicAdd(&s_cur[0][c], 1u);
-      if (s - ga > kBigGroup && q >= S.s0) atomicAdd(&s_cur[1][c], 1u);
+      const uint32_t key = src.ld4(q);
+      const uint32_t b = bin_of(q, key);
+      atomicAdd(&s_cur[0][b], 1u);
+      if (is_target(s, ga, q, key)) atomicAdd(&s_cur[1][b], 1u);
     }
     __syncthreads();
-    if (tid < 2) {
-      uint32_t* st = tid == 0 ? s_cls : s_tcls;
-      uint32_t acc = 0, chunks = 0;
-      for (uint32_t k = 0; k <= kClsNone; k++) {
-        const uint32_t n = s_cur[tid][k];
-        st[k] = acc;
-        s_cur[tid][k] = acc;
-        if (tid == 1) {
-          s_chunk[k] = chunks;
-          chunks += (n + 63) / 64;
-        }
-        acc += n;
+    {
+      uint32_t tc = 0, tt = 0;
+      const uint32_t c0 = tid < kBins ? s_cur[0][tid] : 0u, c1 = tid < kBins ? s_cur[1][tid] : 0u;
+      const uint32_t o0 = block_excl_scan(c0, s_wsum, &tc);
+      const uint32_t o1 = block_excl_scan(c1, s_wsum, &tt);
+      if (tid < kBins) {
+        s_cls[tid] = o0;
+        s_tcls[tid] = o1;
+        s_cur[0][tid] = o0;
+        s_cur[1][tid] = o1;
       }
-      st[kClsNone + 1] = acc;
-      if (tid == 1) {
-        s_chunk[kClsNone + 1] = chunks;
+      if (tid == 0) {
+        s_cls[kBins] = tc;
+        s_tcls[kBins] = tt;
         s_next = 0;
       }
     }
@@ -2254,17 +2308,24 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
       const uint32_t r = slot_pos(compact, small, s);
       const uint64_t q = S.w0 + r;
-      const uint32_t c = cls_of(q);
-      C[ga + atomicAdd(&s_cur[0][c], 1u)] = (c << 17) | r;
-      if (s - ga > kBigGroup && q >= S.s0) T[ga + atomicAdd(&s_cur[1][c], 1u)] = r;
+      const uint32_t key = src.ld4(q);
+      const uint32_t b = bin_of(q, key);
+      C[ga + atomicAdd(&s_cur[0][b], 1u)] = (b << 17) | r;
+      if (is_target(s, ga, q, key)) T[ga + atomicAdd(&s_cur[1][b], 1u)] = (b << 17) | r;
     }
     __threadfence_block();
     __syncthreads();
 
-    // 2. LM of every big target: chunks of up to 64 targets, taken class by class; a class's last,
-    //    partial chunk is filled up with the next classes' first targets (mixed: scan all, filter)
-    const uint32_t nT = s_tcls[kClsNone + 1];
+    // 2. LM of every big target, chunks of 64 targets in bin order.  A lane scans a range of C:
+    //    non-run key: every non-run bin but its own class (p's predecessor is a target of this block:
+    //      those candidates carry from p-1);
+    //    run interior (p-1 in the run): p-1 gives R(p) at distance 1, so only the run STARTS of its R
+    //      bin can do better (R bytes + the next ones); with R(p) >= limit nothing can;
+    //    run start: its R bin (one member per earlier run at least R long, the nearest position of
+    //      that run with R in common); when none is usable, every run member (fallback).
+    const uint32_t nT = s_tcls[kBins];
     const uint32_t nChunks = (nT + 63) / 64;
+    const uint32_t runLo = s_cls[kBinRun0], runHi = s_cls[kBins];
     while (true) {
       uint32_t item = 0;
       if (lane == 0) item = atomicAdd(&s_next, 1u);
@@ -2272,64 +2333,92 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       if (item >= nChunks) break;
       const uint32_t t = item * 64 + lane;
       const bool act = t < nT;
-      const uint32_t pRel = act ? T[ga + t] : 0u;
+      const uint32_t te = act ? T[ga + t] : 0u;
+      const uint32_t pRel = te & 0x1FFFFu, myBin = act ? te >> 17 : kNoBin;
       const uint64_t p = S.w0 + pRel;
-      const uint32_t myCls = act ? cls_of(p) : kClsNone + 1;
-      // p's own class is excluded only when p-1 is a target of this block (its result carries to p)
-      const uint32_t exCls = act && p > B.start && myCls < kClsNone ? myCls : kClsNone + 1;
       const uint32_t me0 = act ? src.ld4(p) : 0u, me1 = act ? src.ld4(p + 4) : 0u, me2 = act ? src.ld4(p + 8) : 0u;
       const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
       const uint32_t limit = room < kLongCap9 ? room : kLongCap9;
       const uint32_t cap12 = limit < 12u ? limit : 12u;
       const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
-      // candidate ranges of C: one class for the whole wavefront -> skip it; else scan everything
-      const uint32_t e0 = rdlane(exCls, 0);
-      const bool one = __ballot(act && exCls != e0) == 0 && e0 < kClsNone;
-      uint32_t r0a = ga, r0b = gb, r1a = gb, r1b = gb;
-      if (one) {
-        r0b = ga + s_cls[e0];
-        r1a = ga + s_cls[e0 + 1];
+      const bool isRun = act && myBin >= kBinRun0;
+      const uint32_t rb = isRun ? (myBin - kBinRun0) >> 1 : 0u;
+      const bool runStart = isRun && ((myBin - kBinRun0) & 1u);
+      const uint32_t R = isRun ? rb + 4u : 0u;
+      uint32_t bestKey = 0, lo = 0, hi = 0, exBin = kNoBin;
+      if (act && !isRun) {
+        lo = 0;
+        hi = runLo;
+        // p's own class is excluded only when p-1 is a target of this block (its result carries to p)
+        if (p > B.start && myBin < kClsNone) exBin = myBin;
+      } else if (isRun && !runStart) {
+        bestKey = ((R < limit ? R : limit) << 17) | (pRel - 1u);
+        if (R < limit) {
+          lo = s_cls[myBin + 1];
+          hi = s_cls[myBin + 2];
+        }
+      } else if (runStart) {
+        lo = s_cls[myBin - 1];
+        hi = s_cls[myBin + 1];
       }
-      uint32_t bestKey = 0;
-      for (int part = 0; part < 2; part++) {
-        const uint32_t lo = part == 0 ? r0a : r1a, hi = part == 0 ? r0b : r1b;
-        for (uint32_t base = lo; base < hi; base += 64) {
-          const uint32_t ci = base + lane;
-          const uint32_t ce = ci < hi ? C[ci] : 0xFFFFFFFFu;
-          const uint32_t cr = ce & 0x1FFFFu;
-          const uint64_t cp = S.w0 + (ci < hi ? cr : 0u);
-          const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
-          const uint32_t n = hi - base < 64u ? hi - base : 64u;
-          for (uint32_t j = 0; j < n; j++) {
-            const uint32_t ej = rdlane(ce, j), k0 = rdlane(f0, j), k1 = rdlane(f1, j), k2 = rdlane(f2, j);
-            const uint32_t c = ej & 0x1FFFFu;
-            const bool ok = act && c < pRel && c >= lbRel && (ej >> 17) != exCls && k0 == me0;
-            const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
-            const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
-            const uint32_t z = min(z1, 32u + min(z2, 32u));
-            uint32_t lcp = min(4u + (z >> 3), cap12);
-            if (ok && lcp == 12u && limit > 12u) {
-              // both share 12 bytes: the exact prefix, unless the 4 bytes ending at the current best
-              // length already differ (then it stays below the best and cannot win)
-              const uint64_t cc = S.w0 + c;
-              const uint32_t bl = bestKey >> 17;
-              bool open = !(bl > 12u && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
-              while (open && lcp < limit) {
-                const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
-                if (x) {
-                  lcp += (uint32_t)__builtin_ctz(x) >> 3;
-                  open = false;
-                } else {
-                  lcp += 4;
-                }
-              }
-              if (lcp > limit) lcp = limit;
+      // one candidate for the lanes whose range holds C index ci: entry ej, first 12 bytes k0..k2
+      auto take = [&](uint32_t ci, uint32_t clo, uint32_t chi, uint32_t ej, uint32_t k0, uint32_t k1, uint32_t k2) {
+        const uint32_t c = ej & 0x1FFFFu, cb = ej >> 17;
+        const bool ok = ci >= clo && ci < chi && cb != exBin && c < pRel && c >= lbRel && k0 == me0;
+        const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        uint32_t lcp = min(4u + (z >> 3), cap12);
+        if (ok && lcp == 12u && limit > 12u) {
+          // both share 12 bytes (a member of p's own R bin shares R): the exact prefix, unless the 4
+          // bytes ending at the current best length already differ (then it cannot win)
+          const uint64_t cc = S.w0 + c;
+          const uint32_t bl = bestKey >> 17;
+          if (isRun && cb >= kBinRun0 && ((cb - kBinRun0) >> 1) == rb) lcp = max(12u, min(R, limit));
+          bool open = !(bl > lcp && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
+          while (open && lcp < limit) {
+            const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
+            if (x) {
+              lcp += (uint32_t)__builtin_ctz(x) >> 3;
+              open = false;
+            } else {
+              lcp += 4;
             }
-            const uint32_t key = ok ? (lcp << 17) | c : 0u;
-            bestKey = key > bestKey ? key : bestKey;
+          }
+          if (lcp > limit) lcp = limit;
+        }
+        const uint32_t key = ok ? (lcp << 17) | c : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+      };
+      // the wave scans the union of its lanes' ranges; a wave of one class skips that class's bin
+      auto scan = [&](uint32_t clo, uint32_t chi) {
+        const uint32_t wlo = wave_min_u32(clo < chi ? clo : 0xFFFFFFFFu);
+        const uint32_t whi = 0xFFFFFFFFu - wave_min_u32(clo < chi ? 0xFFFFFFFFu - chi : 0xFFFFFFFFu);
+        if (wlo >= whi) return;
+        const uint32_t e0 = rdlane(exBin, (uint32_t)__builtin_ctzll(__ballot(act) | (1ull << 63)));
+        const bool one = e0 != kNoBin && __ballot(act && exBin != e0) == 0;
+        uint32_t r0a = wlo, r0b = whi, r1a = whi, r1b = whi;
+        if (one) {
+          r0b = min(whi, s_cls[e0]);
+          r1a = max(wlo, s_cls[e0 + 1]);
+        }
+        for (int part = 0; part < 2; part++) {
+          const uint32_t a = part == 0 ? r0a : r1a, b = part == 0 ? r0b : r1b;
+          for (uint32_t base = a; base < b; base += 64) {
+            const uint32_t ci = base + lane;
+            const uint32_t ce = ci < b ? C[ga + ci] : 0xFFFFFFFFu;
+            const uint64_t cp = S.w0 + (ci < b ? ce & 0x1FFFFu : 0u);
+            const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
+            const uint32_t n = b - base < 64u ? b - base : 64u;
+            for (uint32_t j = 0; j < n; j++)
+              take(base + j, clo, chi, rdlane(ce, j), rdlane(f0, j), rdlane(f1, j), rdlane(f2, j));
           }
         }
-      }
+      };
+      scan(lo, hi);
+      // run starts with no usable member of their R bin: every run member
+      const bool fb = runStart && bestKey == 0u;
+      if (__ballot(fb)) scan(fb ? runLo : 0u, fb ? runHi : 0u);
       if (act) {
         const uint32_t bl = bestKey >> 17;
         lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (uint32_t)(pRel - (bestKey & 0x1FFFFu)) : 0u;

@@ -34,6 +34,12 @@ def make(spec: dict) -> bytes:
         data = synth.small_alphabet(spec["n"], k=spec["k"], seed=spec["seed"])
     elif kind == "runs":
         data = synth.runs(spec["n"], seed=spec["seed"], max_run=spec.get("max_run", 3000))
+    elif kind == "silesia_piece":
+        data = synth._silesia_piece((spec["kind"], spec["n"], spec["seed"], spec.get("index", 0)))
+    elif kind == "silesia_like":
+        data = synth.silesia_like(spec["n"], seed=spec["seed"], workers=spec.get("workers", 1))
+    elif kind == "zeros_urandom_range":
+        data = synth.zeros_urandom_range(spec["lo"], spec["lo"] + spec["n"], seed=spec["seed"])
     elif kind == "concat":
         data = b"".join(make(p) for p in spec["parts"])
     else:

@@ -110,6 +110,32 @@ def test_blocks_silesia_mix_4m(compressor):
     assert compressor.compress_blocks(data, 4 << 20, 65535) == expected_frame(data, 4 << 20, 65535)
 
 
+def _blocks_golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "blocks.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", _blocks_golden(), ids=lambda c: c["name"])
+def test_blocks_golden_fixtures(compressor, case):
+    """Full-size blocks the reference is too slow to redo inside a test (4 MiB blocks of binary
+    records: ~2 minutes each at -9): every block's bytes against the reference's own output,
+    recorded by tests/golden/make_blocks_golden.py.  Covers each Silesia kind at configs[2]'s 4 MiB,
+    run-key groups (k_find_big's run bins) at 64 KiB / 256 KiB / 4 MiB, and configs[4]'s zeros/urandom
+    layout at 256 KiB."""
+    data = inputs.make(case["input"])
+    assert inputs.sha(data) == case["input_sha256"]
+    frame = compressor.compress_blocks(data, case["block_size"], case["max_chain"])
+    assert len(frame) == case["frame_len"]
+    pos, bad = 7, []
+    for i, (want, n) in enumerate(zip(case["block_sha256"], case["block_len"])):
+        if inputs.sha(frame[pos:pos + n]) != want:
+            bad.append(i)
+        pos += n
+    assert not bad, f"blocks differing from the reference: {bad}"
+    assert pyoracle.oz_unlz4(frame, cap=len(data) + 16) == data
+
+
 def _skip_into_run(seed):
     """A long match that ends 10 bytes into a 100 KB zero run: at greedy/lazy levels the run's first
     positions are skipped, so the same-letter shortcut starts later than the run."""

@@ -53,6 +53,21 @@ def test_golden_covers_every_level_and_mode(golden):
     assert any(c["input_len"] == 0 for c in golden)
 
 
+def test_blocks_golden_inputs_unchanged():
+    """tests/golden/blocks.json (independent-block fixtures of the reference, checked on the GPU by
+    test_gpu.py::test_blocks_golden_fixtures): the generators still produce the recorded inputs."""
+    import json
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "blocks.json")) as f:
+        cases = json.load(f)["cases"]
+    assert {"db_4m", "xml_4m", "exe_4m", "image_4m", "src_4m", "text_4m", "zu_256k"} <= {c["name"] for c in cases}
+    for case in cases:
+        data = inputs.make(case["input"])
+        assert inputs.sha(data) == case["input_sha256"], case["name"]
+        nb = (len(data) + case["block_size"] - 1) // case["block_size"]
+        assert len(case["block_sha256"]) == len(case["block_len"]) == nb
+        assert case["frame_len"] == 11 + sum(case["block_len"])
+
+
 @pytest.mark.skipif(not pyoracle.ref_available(), reason="reference not compiled (oracle/_ref)")
 @pytest.mark.parametrize("seed", range(6))
 def test_oracle_matches_reference_random(seed):
