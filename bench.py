@@ -9,9 +9,11 @@ workloads (BASELINE.json configs; all synthetic, the corpora are not available o
   enwik9        configs[3]: an enwik9-shaped input (10^9 bytes at 8 GPUs) in 64 KiB blocks, sharded:
                 rank r of N compresses its contiguous block range of the first N x 125 MB, so every
                 GPU does the same work at any N (weak scaling) and N=8 is the whole 10^9 bytes.  The
-                default at N>1.
-  zeros_urandom configs[4]: 10 GiB of alternating 128 KiB zero / urandom runs at 8 GPUs, 256 KiB
-                blocks, sharded the same way (1.25 GiB per GPU).
+                default at N>1; at N=1 the `shapes` leg measures the same 125 MB per GPU, so a 1->8
+                curve can be read on one workload.
+  zeros_urandom configs[4]: 10 GiB of zero and urandom runs of random lengths (mean 128 KiB, 50/50
+                bytes, runs straddling the block grid) at 8 GPUs, 256 KiB blocks, sharded the same way
+                (1.25 GiB per GPU).
   silesia       configs[2]: Silesia-shaped mixed content (text, XML, executables, database rows,
                 images, source), 4 MiB independent blocks, 1 GPU.
 One step = one full compression of the rank's shard, input resident in HBM, blocks written to HBM.
@@ -25,15 +27,20 @@ this process touches the GPU) and exits with its status.
 
 Also reported:
   byte_diff      differing bytes between the GPU blocks and the reference's output for the same
-                 blocks (oracle/_ref, compiled from the reference sources; the C restatement when
-                 _ref is absent): every block at N=1 on enwik8, a fixed per-rank sample otherwise
+                 blocks (oracle/_ref/smallz4, the reference CLI compiled from its sources, one child
+                 process per block with a hard deadline; the C restatement when _ref is absent):
+                 every block at N=1 on enwik8, otherwise a seeded random sample bounded by
+                 --verify-seconds
   roundtrip      every rank's part decoded on the device (sz4_unlz4_device) equals its input
   roofline       dominant kernel (k_find_sorted), HIP-event timed on its stream; HBM traffic from the
                  newest matching profiles/*_pmc.json (rocprofv3 PMC passes of the same workload)
-  cpu_baseline   the reference itself on this host: all 16 host threads of the box's share, and one
-                 thread, on a bounded sample
+  cpu_baseline   the reference itself on this host (rank 0, every N, after the timed region): all 16
+                 host threads of the box's share, and one thread, on a bounded sample
   stream         sz4_lz4 (the drop-in's host-buffer path: 4 MiB dependent blocks, chunked, PCIe
-                 included), 1 GPU, outside the timed region
+                 included) between numpy buffers, 1 GPU, outside the timed region
+  shapes         N=1: the other single-GPU-sized configs -- configs[2] (Silesia-shaped, 4 MiB blocks),
+                 configs[4]'s 1.25 GiB rank slice, text at 4 MiB blocks, configs[3]'s 125 MB rank slice
+                 -- each with ms/step, MB/s, a sampled byte_diff bounded by seconds, and the round trip
 """
 from __future__ import annotations
 
@@ -64,19 +71,24 @@ WORKLOADS = {
                lambda lo, hi: synth.enwik8_like(100_000_000, seed=8)[lo:hi]),
     "enwik9": ("configs[3]", "synthetic enwik9-shaped text: 16 MiB enwik8-shaped segments (synth.enwik9_like_range)",
                65536, lambda world: 125_000_000,
-               lambda lo, hi: synth.enwik9_like_range(lo, hi, seed=9, workers=4)),
-    "zeros_urandom": ("configs[4]", "synthetic: alternating 128 KiB runs of zeros and urandom bytes (synth.zeros_urandom_range)",
+               lambda lo, hi: synth.enwik9_like_range(lo, hi, seed=9, workers=HOST_THREADS)),
+    "zeros_urandom": ("configs[4]", "synthetic: zero and urandom runs of random lengths, mean 128 KiB, 50/50 bytes "
+                                    "(synth.zeros_urandom_range)",
                       262144, lambda world: (10 << 30) // 8,
                       lambda lo, hi: synth.zeros_urandom_range(lo, hi, seed=10)),
     "silesia": ("configs[2]", "synthetic Silesia-shaped mixed content (synth.silesia_like; the corpus is not available offline)",
                 4 << 20, lambda world: 211_938_580,
-                lambda lo, hi: synth.silesia_like(hi, seed=2)[lo:hi]),
+                lambda lo, hi: synth.silesia_like(hi, seed=2, workers=HOST_THREADS)[lo:hi]),
     # diagnostic shapes (not BASELINE configs): the kernels' floors on incompressible / all-run data
     "random": ("diagnostic", "synthetic: urandom bytes (numpy, seeded)", 65536, lambda world: 100_000_000,
                lambda lo, hi: synth.random_bytes(hi, seed=8)[lo:hi]),
     "zeros": ("diagnostic", "synthetic: all zero bytes", 65536, lambda world: 100_000_000,
               lambda lo, hi: bytes(hi - lo)),
 }
+
+# the shapes leg at N=1: (label, workload, block size override)
+SHAPES = [("silesia_4m", "silesia", None), ("zeros_urandom_256k", "zeros_urandom", None),
+          ("enwik8_4m", "enwik8", 4 << 20), ("enwik9_rank_slice", "enwik9", None)]
 
 
 def parse_args(argv=None):
@@ -91,11 +103,15 @@ def parse_args(argv=None):
     ap.add_argument("--level", type=int, default=9)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU baseline sample")
     ap.add_argument("--verify-threads", type=int, default=HOST_THREADS)
-    ap.add_argument("--verify-blocks", type=int, default=256,
-                    help="per-rank sample of blocks diffed against the reference (0 = every block)")
+    ap.add_argument("--verify-seconds", type=float, default=20.0,
+                    help="per-rank budget of the sampled byte diff against the reference (the whole "
+                         "input at N=1 on enwik8 is always diffed)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the device round trip (sz4_unlz4_device)")
     ap.add_argument("--no-stream", action="store_true", help="skip the sz4_lz4 host-buffer leg")
+    ap.add_argument("--no-shapes", action="store_true", help="skip the other configs (N=1)")
+    ap.add_argument("--shape-steps", type=int, default=3)
+    ap.add_argument("--shape-verify-seconds", type=float, default=8.0)
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks compress their shards with the oracle (tests the sharding)")
     a = ap.parse_args(argv)
@@ -104,29 +120,15 @@ def parse_args(argv=None):
     return a
 
 
-def rank_range(args, world, rank):
+def rank_range(args, world, rank, workload=None, block_size=None, mb=None):
     """(global input length, [lo, hi) of this rank, block size)."""
-    wl = WORKLOADS[args.workload]
-    bs = args.block_size or wl[2]
-    per = int(args.mb * 1e6) if args.mb else wl[3](world)
+    wl = WORKLOADS[workload or args.workload]
+    bs = block_size or args.block_size or wl[2]
+    mb = mb if mb is not None else args.mb
+    per = int(mb * 1e6) if mb else wl[3](world)
     total = per * world
     lo, hi = shard.shard_range(total, bs, rank, world)
     return total, lo, hi, bs
-
-
-def expected_blocks(data: bytes, bs: int, chain: int, threads: int, offsets):
-    """Reference output (block word + payload) of the blocks starting at `offsets`, on the CPU."""
-    from oracle import pyoracle
-    if pyoracle.ref_available():
-        def one(off):
-            return pyoracle.ref_lz4(data[off:off + bs], chain)[7:-4]
-        kind = "reference"
-    else:
-        def one(off):
-            return pyoracle.oz_block(data[off:off + bs], chain)
-        kind = "port"
-    with ThreadPoolExecutor(max_workers=threads) as ex:
-        return list(ex.map(one, offsets)), kind
 
 
 def block_spans(part: bytes):
@@ -140,23 +142,58 @@ def block_spans(part: bytes):
     return spans
 
 
-def sample_diff(part: bytes, data: bytes, bs: int, chain: int, threads: int, sample: int):
-    """Byte diff of a fixed sample of this rank's blocks (every k-th) against the reference."""
+def _level_flag(chain: int) -> str:
+    return "-9" if chain >= 65535 else f"-{chain}"
+
+
+def verify_sample(part: bytes, data: bytes, bs: int, chain: int, threads: int, budget_s: float, every: bool):
+    """Byte diff of this rank's blocks against the reference.  Blocks are taken in a seeded random
+    order (all of them when `every`), each compressed by the reference CLI (oracle/_ref/smallz4) in a
+    child process that is killed at the deadline, so the leg is bounded by `budget_s` whatever one
+    block costs the reference (4 MiB of binary records: ~2 minutes at -9)."""
+    import numpy as np
+    from oracle import pyoracle
     spans = block_spans(part)
     nblk = (len(data) + bs - 1) // bs
     if len(spans) != nblk:
-        return len(part) + 1, 0, None
-    step = 1 if sample <= 0 or nblk <= sample else nblk // sample
-    idx = list(range(0, nblk, step))
-    want, kind = expected_blocks(data, bs, chain, threads, [i * bs for i in idx])
-    diff = 0
-    for i, w in zip(idx, want):
-        o, n = spans[i]
-        got = part[o:o + n]
-        m = min(len(got), len(w))
-        diff += sum(1 for a, b in zip(got[:m], w[:m]) if a != b) if got != w else 0
-        diff += abs(len(got) - len(w))
-    return diff, len(idx), kind
+        return {"byte_diff": len(part) + 1, "blocks_verified": 0, "blocks_total": nblk, "verified_against": None,
+                "note": "block count differs"}
+    order = list(range(nblk)) if every else [int(i) for i in np.random.default_rng(2024).permutation(nblk)]
+    cli = os.path.join(ROOT, "oracle", "_ref", "smallz4")
+    use_cli = os.path.exists(cli)
+    kind = "reference" if use_cli else "port"
+    t0 = time.perf_counter()
+    deadline = t0 + budget_s
+
+    def one(i):
+        block = data[i * bs:(i + 1) * bs]
+        left = deadline - time.perf_counter()
+        if left <= 0.05:
+            return i, None
+        if use_cli:
+            try:
+                r = subprocess.run([cli, _level_flag(chain), "-f"], input=block, capture_output=True, timeout=left)
+            except subprocess.TimeoutExpired:
+                return i, None
+            if r.returncode != 0:
+                return i, b""
+            return i, r.stdout[7:-4]
+        return i, pyoracle.oz_block(block, chain)
+
+    diff, done = 0, 0
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        for i, want in ex.map(one, order):
+            if want is None:
+                continue
+            o, n = spans[i]
+            got = part[o:o + n]
+            if got != want:
+                m = min(len(got), len(want))
+                diff += sum(1 for a, b in zip(got[:m], want[:m]) if a != b) + abs(len(got) - len(want))
+            done += 1
+    return {"byte_diff": diff, "blocks_verified": done, "blocks_total": nblk, "verified_against": kind,
+            "verify_seconds": round(time.perf_counter() - t0, 2), "verify_budget_s": budget_s,
+            "verify_sample": "every block" if every else "seeded random order, cut at the budget"}
 
 
 def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
@@ -191,10 +228,11 @@ def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
 
 
 def pmc_traffic(cfg):
-    """HBM bytes per k_find_sorted launch from the newest profiles/*_pmc.json of this workload."""
+    """HBM bytes per k_find_sorted launch from the newest profiles/**/*_pmc.json of this workload."""
     best = None
     # tags run r02a..r02z, r02aa..r02az: order by tag length first so r02av sorts after r02o
-    paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json"))
+    paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")) + \
+        glob.glob(os.path.join(ROOT, "profiles", "*", "*_pmc.json"))
     for path in sorted(paths, key=lambda p: (len(os.path.basename(p)), os.path.basename(p))):
         try:
             with open(path) as f:
@@ -222,7 +260,8 @@ def spawn_ranks(args):
 
 def dry_run(args, world, rank):
     """HIP-free rehearsal of the sharded path (gloo): each rank compresses its block range with the
-    oracle; rank 0 checks that the parts concatenate to the single-process frame."""
+    oracle; rank 0 checks that the parts concatenate to the single-process frame, and reports the
+    fields the GPU line would carry (workload, cpu_baseline, verify budget)."""
     import torch.distributed as dist
     from oracle import pyoracle
     if world > 1:
@@ -237,10 +276,122 @@ def dry_run(args, world, rank):
         whole = WORKLOADS[args.workload][4](0, total)
         single = shard.HEADER + b"".join(pyoracle.oz_block(whole[o:o + bs], chain)
                                          for o in range(0, total, bs)) + shard.END_MARK
-        print(json.dumps({"dry_run": True, "n_gpus": world, "workload": args.workload, "input_bytes": total,
-                          "frame_bytes": len(frame), "parts_equal_single": frame == single}), flush=True)
+        rec = {"dry_run": True, "n_gpus": world, "workload": args.workload, "input_bytes": total,
+               "bytes_per_gpu": hi - lo, "frame_bytes": len(frame), "parts_equal_single": frame == single,
+               "verify_budget_s": args.verify_seconds,
+               "cpu_baseline": cpu_baseline(data, bs, chain, min(args.cpu_seconds, 0.5))}
+        print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+class Runner:
+    """One rank's GPU state: the compressor context, its device and stream."""
+
+    def __init__(self, local):
+        import torch
+        import smallz4_amd
+        self.torch = torch
+        self.local = local
+        self.dev = f"cuda:{local}"
+        self.comp = smallz4_amd.Compressor(device=local)
+        self.stream = torch.cuda.current_stream(local).cuda_stream
+
+    def compress(self, data: bytes, bs: int, chain: int, steps: int, warmup: int, header: str, barrier=None):
+        """Timed compression of `data` (resident in HBM): (seconds of `steps` steps, mean stage ms,
+        frame bytes, the frame tensor, the input tensor)."""
+        torch = self.torch
+        n = len(data)
+        t_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(self.dev) if n else \
+            torch.empty(0, dtype=torch.uint8, device=self.dev)
+        cap = self.comp._lib.sz4_bound(n, bs)
+        out = torch.empty(max(cap, 16), dtype=torch.uint8, device=self.dev)
+
+        def step():
+            return self.comp.compress_blocks_device(t_in.data_ptr() if n else out.data_ptr(), n, out.data_ptr(), cap,
+                                                    bs, chain, header, self.stream)
+
+        self.comp.set_timing(True)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(self.local)
+        if barrier:
+            barrier()
+        torch.cuda.synchronize(self.local)
+        t0 = time.perf_counter()
+        stage_sum, size = {}, 0
+        for _ in range(steps):
+            size = step()
+            for k, v in self.comp.last_stage_ms().items():
+                stage_sum[k] = stage_sum.get(k, 0.0) + v
+        torch.cuda.synchronize(self.local)
+        if barrier:
+            barrier()
+        torch.cuda.synchronize(self.local)
+        elapsed = time.perf_counter() - t0
+        return elapsed, {k: v / max(steps, 1) for k, v in stage_sum.items()}, size, out, t_in
+
+    def roundtrip(self, out, size: int, header: str, t_in, reps: int = 3):
+        """Decode this rank's blocks on the device (sz4_unlz4_device): (equal to the input, timing)."""
+        torch = self.torch
+        n = t_in.numel()
+        if not n:
+            return True, None
+        off = 7 if header == "smallz4" else 0
+        nbody = size - off - (4 if header == "smallz4" else 0)
+        fr = torch.empty(nbody + 11, dtype=torch.uint8, device=self.dev)
+        fr[:7] = torch.tensor(list(shard.HEADER), dtype=torch.uint8)
+        fr[7:7 + nbody] = out[off:off + nbody]
+        fr[7 + nbody:] = 0
+        dout = torch.empty(n, dtype=torch.uint8, device=self.dev)
+        self.comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), n, stream=self.stream)
+        torch.cuda.synchronize(self.local)
+        td = time.perf_counter()
+        got = 0
+        for _ in range(reps):
+            got = self.comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), n, stream=self.stream)
+        torch.cuda.synchronize(self.local)
+        dt = (time.perf_counter() - td) / reps
+        ok = bool(got == n and torch.equal(dout, t_in))
+        del dout, fr
+        return ok, {"value": round(n / dt / 1e6, 1), "unit": "MB/s of decoded output (host-timed call: index, sizes "
+                    "and decode launches with their syncs)", "ms": round(dt * 1e3, 3)}
+
+
+def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
+    """The other single-GPU-sized configs, each measured, diffed on a bounded sample and round-tripped."""
+    torch = run.torch
+    res = {}
+    for label, wl, bso in SHAPES:
+        t0 = time.perf_counter()
+        total, lo, hi, bs = rank_range(args, 1, 0, workload=wl, block_size=bso, mb=0)
+        if wl == "enwik8" and enwik8_data is not None and len(enwik8_data) == hi - lo:
+            data = enwik8_data
+        elif wl == "enwik9":
+            # configs[3]'s rank-0 slice at N=8: the same 125 MB every rank compresses at any N
+            total, lo, hi, bs = rank_range(args, 8, 0, workload=wl, mb=0)
+            data = WORKLOADS[wl][4](lo, hi)
+        else:
+            data = WORKLOADS[wl][4](lo, hi)
+        gen_s = time.perf_counter() - t0
+        steps = args.shape_steps
+        elapsed, stages, size, out, t_in = run.compress(data, bs, chain, steps, 1, "none")
+        part = out[:size].cpu().numpy().tobytes()
+        rt_ok, _ = run.roundtrip(out, size, "none", t_in, reps=1)
+        del out, t_in
+        torch.cuda.empty_cache()
+        rec = {"config": f"{wl} ({WORKLOADS[wl][0]}): {len(data) / 1e6:g} MB as independent {bs}-byte blocks, "
+                         f"level -{args.level}", "baseline_config": WORKLOADS[wl][0], "block_size": bs,
+               "input_bytes": len(data), "MB/s": round(len(data) * steps / elapsed / 1e6, 2),
+               "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": 1,
+               "compression_ratio": round((size + 11) / len(data), 5), "roundtrip_ok": rt_ok,
+               "stages_ms": {k: round(v, 3) for k, v in stages.items()}, "generate_s": round(gen_s, 1)}
+        if not args.no_verify:
+            rec.update(verify_sample(part, data, bs, chain, args.verify_threads, args.shape_verify_seconds, every=False))
+        res[label] = rec
+        print(json.dumps({"shape": label, **rec}), file=sys.stderr, flush=True)
+        del data, part
+    return res
 
 
 def main():
@@ -277,73 +428,30 @@ def main():
     total, lo, hi, bs = rank_range(args, world, rank)
     nbytes = hi - lo
     data = WORKLOADS[args.workload][4](lo, hi)
-    dev = f"cuda:{local}"
-    t_in = torch.frombuffer(bytearray(data), dtype=torch.uint8).to(dev) if nbytes else torch.empty(0, dtype=torch.uint8, device=dev)
-    comp = smallz4_amd.Compressor(device=local)
-    cap = comp._lib.sz4_bound(nbytes, bs)
-    out = torch.empty(max(cap, 16), dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(local).cuda_stream
+    run = Runner(local)
     # rank 0 writes the smallz4 header, the last rank the end mark, the others bare blocks
     header = "smallz4" if world == 1 else "none"
-
-    def step():
-        return comp.compress_blocks_device(t_in.data_ptr(), nbytes, out.data_ptr(), cap, bs, chain, header, stream)
-
-    comp.set_timing(True)
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(local)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(local)
-    t0 = time.perf_counter()
-    stage_sum = {}
-    size = 0
-    for _ in range(args.steps):
-        size = step()
-        for k, v in comp.last_stage_ms().items():
-            stage_sum[k] = stage_sum.get(k, 0.0) + v
-    torch.cuda.synchronize(local)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(local)
-    elapsed = time.perf_counter() - t0
-    stages = {k: v / args.steps for k, v in stage_sum.items()}
+    barrier = dist.barrier if world > 1 else None
+    elapsed, stages, size, out, t_in = run.compress(data, bs, chain, args.steps, args.warmup, header, barrier)
     part = out[:size].cpu().numpy().tobytes()
     blocks = part[7:-4] if header == "smallz4" else part
 
-    # device round trip of this rank's part (outside the timed region): wrap the bare blocks as a
-    # frame on the device, decode with sz4_unlz4_device, compare with the input in HBM
+    # device round trip of this rank's part (outside the timed region)
     rt_ok, dec = True, None
     if not args.no_decode and nbytes:
-        fr = torch.empty(len(blocks) + 11, dtype=torch.uint8, device=dev)
-        fr[:7] = torch.tensor(list(shard.HEADER), dtype=torch.uint8)
-        off = 7 if header == "smallz4" else 0
-        fr[7:7 + len(blocks)] = out[off:off + len(blocks)]
-        fr[7 + len(blocks):] = 0
-        dout = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), nbytes, stream=stream)
-        torch.cuda.synchronize(local)
-        reps = 3
-        td = time.perf_counter()
-        for _ in range(reps):
-            got = comp.unlz4_device(fr.data_ptr(), fr.numel(), dout.data_ptr(), nbytes, stream=stream)
-        torch.cuda.synchronize(local)
-        dt = (time.perf_counter() - td) / reps
-        rt_ok = bool(got == nbytes and torch.equal(dout, t_in))
-        dec = {"value": round(nbytes / dt / 1e6, 1), "unit": "MB/s of decoded output (rank 0; host-timed call: "
-               "index, sizes and decode launches with their syncs)", "ms": round(dt * 1e3, 3)}
-        del dout, fr
+        rt_ok, dec = run.roundtrip(out, size, header, t_in)
+    del out, t_in
+    torch.cuda.empty_cache()
 
-    # output-byte diff against the reference on a sample of this rank's blocks (all at N=1 on enwik8)
-    diff, verified, kind = -1, 0, None
+    # output-byte diff against the reference: every block at N=1 on enwik8, else a sample bounded in time
+    ver = {"byte_diff": -1, "blocks_verified": 0, "verified_against": None}
     if not args.no_verify and nbytes:
-        sample = 0 if (world == 1 and args.workload == "enwik8") else args.verify_blocks
-        diff, verified, kind = sample_diff(blocks, data, bs, chain, args.verify_threads, sample)
+        every = world == 1 and args.workload == "enwik8"
+        ver = verify_sample(blocks, data, bs, chain, args.verify_threads, 600.0 if every else args.verify_seconds, every)
 
     # whole-job results over ranks
-    res = torch.tensor([elapsed, float(size), float(diff), float(verified), 0.0 if rt_ok else 1.0],
-                       dtype=torch.float64, device="cpu" if share else dev)
+    res = torch.tensor([elapsed, float(size), float(ver["byte_diff"]), float(ver["blocks_verified"]),
+                        0.0 if rt_ok else 1.0], dtype=torch.float64, device="cpu" if share else f"cuda:{local}")
     if world > 1:
         mx = res.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -353,20 +461,28 @@ def main():
         diff = -1 if float(mx[2]) < 0 else int(res[2])
         verified, rt_bad = int(res[3]), int(res[4])
     else:
-        frame_bytes, rt_bad = size, 0 if rt_ok else 1
+        frame_bytes, diff, verified, rt_bad = size, ver["byte_diff"], ver["blocks_verified"], 0 if rt_ok else 1
 
     stream_leg = None
     if world == 1 and not args.no_stream and nbytes:
-        # the drop-in's host-buffer path (4 MiB dependent blocks, chunked; PCIe included)
-        sdata = data[:min(nbytes, 100_000_000)]
-        comp.lz4(sdata[:1 << 20], chain)
+        # the drop-in's host-buffer path (4 MiB dependent blocks, chunked; PCIe included), between
+        # numpy buffers: no Python copies inside the timed call
+        import numpy as np
+        src = np.frombuffer(data[:min(nbytes, 100_000_000)], dtype=np.uint8)
+        dst = np.empty(run.comp._lib.sz4_lz4_bound(src.size, 0), dtype=np.uint8)
+        run.comp.lz4_into(src[:1 << 20], dst, chain)
         ts = time.perf_counter()
-        sframe = comp.lz4(sdata, chain)
+        ssize = run.comp.lz4_into(src, dst, chain)
         dts = time.perf_counter() - ts
-        stream_leg = {"value": round(len(sdata) / dts / 1e6, 1), "unit": "MB/s (host buffers in and out, PCIe included)",
-                      "input_bytes": len(sdata), "ratio": round(len(sframe) / len(sdata), 5),
-                      "path": "sz4_lz4: smallz4::lz4 stream semantics, 4 MiB dependent blocks, 64 MiB chunks",
-                      "device_bytes": comp.device_bytes()}
+        stream_leg = {"value": round(src.size / dts / 1e6, 1), "unit": "MB/s (host buffers in and out, PCIe included)",
+                      "input_bytes": int(src.size), "ratio": round(ssize / src.size, 5),
+                      "path": "sz4_lz4 (smallz4::lz4 stream semantics: 4 MiB dependent blocks, 64 MiB chunks) "
+                              "between numpy buffers",
+                      "device_bytes": run.comp.device_bytes()}
+
+    shapes = None
+    if world == 1 and not args.no_shapes and args.level == 9 and args.workload == "enwik8" and not args.mb:
+        shapes = shapes_leg(args, run, chain, data)
 
     if rank == 0:
         wl = WORKLOADS[args.workload]
@@ -394,8 +510,8 @@ def main():
                 "limiter": "instruction issue and latency (VALU candidate checks, SALU control): achieved/peak is "
                            "the HBM roofline (algorithmic bytes per launch / launch time vs 8 TB/s), the issue "
                            "roofline is under 'issue'",
-                "step_compulsory": {"bytes": nbytes + size, "GB/s": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world, 3),
-                                    "frac": round((nbytes + size) / (elapsed / args.steps) / 1e9 / world / HBM_PEAK_GBS, 6),
+                "step_compulsory": {"bytes": nbytes + size, "GB/s": round((nbytes + size) / (elapsed / args.steps) / 1e9, 3),
+                                    "frac": round((nbytes + size) / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 6),
                                     "note": "input read + frame written per GPU per step over the whole step"}}
         if pmc:
             roof["traffic_source"] = os.path.relpath(pmc[0], ROOT)
@@ -426,9 +542,11 @@ def main():
             "dtype": "u8",
             "data": wl[1],
             "config": cfg,
+            "value_per_gpu": round(value / world, 2),
             "byte_diff": diff,
             "blocks_verified": verified,
-            "verified_against": kind,
+            "verified_against": ver.get("verified_against"),
+            "verify": {k: v for k, v in ver.items() if k.startswith("verify") or k == "blocks_total"},
             "roundtrip_ok": rt_bad == 0,
             "compression_ratio": round(frame_bytes / total, 5) if total else None,
             "stages_ms": {k: round(v, 3) for k, v in stages.items()},
@@ -438,8 +556,10 @@ def main():
             rec["unlz4"] = dec
         if stream_leg is not None:
             rec["stream"] = stream_leg
-        if world == 1:
-            rec["cpu_baseline"] = cpu_baseline(data, bs, chain, args.cpu_seconds)
+        if shapes is not None:
+            rec["shapes"] = shapes
+        # the reference on this host's cores, rank 0, after the timed region (at every N)
+        rec["cpu_baseline"] = cpu_baseline(data, bs, chain, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

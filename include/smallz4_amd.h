@@ -63,6 +63,8 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * block_size bytes (last block shorter).  Each block's bytes in the output
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
+ * Any n in bounded memory: the blocks are compressed in pieces of at most
+ * sz4_set_batch_chunk bytes (128 MiB by default, ~10 GB of scratch).
  *
  *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
  *   block_size    1 .. 4 MiB
@@ -106,7 +108,8 @@ typedef void (*sz4_send_bytes)(const void* data, size_t numBytes, void* userPtr)
  * the whole input and the device footprint does not grow with the input.  send_bytes receives the
  * header, then per block four 1-byte calls for the size word followed by the payload, then the end
  * mark: the reference's call pattern (smallz4.h:478-496, 770-780, 807-812).  Both callbacks run on
- * the calling thread; the GPU compresses chunk i while chunk i+1 is read and chunk i-1 is sent.
+ * the calling thread; the GPU compresses chunk i+1 while chunk i is sent and chunk i+2 is read and
+ * uploaded (three HIP streams).  Pinned host buffers grow with the input up to one chunk.
  * A context serves one call at a time (use one context per thread). */
 int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_bytes, uint32_t max_chain,
                    const void* dict, uint64_t dict_len, int legacy, void* user);
@@ -114,6 +117,10 @@ int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_by
 /* Input bytes per chunk of the stream paths (sz4_lz4_stream, sz4_lz4; sz4_unlz4_stream queues half
  * as many frame bytes); rounded down to whole blocks, at least one.  0 restores the 64 MiB default. */
 void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
+
+/* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
+ * device scratch is about 60-75 bytes per piece byte.  0 restores the 128 MiB default. */
+void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured
  * with HIP events on the call's stream.  stage_ms[0..n) receives

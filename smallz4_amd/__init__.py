@@ -84,6 +84,22 @@ class Compressor:
         self._check(rc, "sz4_lz4")
         return out.raw[:size.value]
 
+    def lz4_into(self, src, dst, max_chain_length: int = MaxChainLength, dictionary: bytes = b"",
+                 use_legacy_format: bool = False) -> int:
+        """sz4_lz4 between caller-owned host buffers (numpy uint8 arrays, no Python copies): compresses
+        src into dst (at least sz4_lz4_bound(len(src)) bytes) and returns the frame length."""
+        import numpy as np
+        src = np.ascontiguousarray(src, dtype=np.uint8)
+        if not (isinstance(dst, np.ndarray) and dst.dtype == np.uint8 and dst.flags.c_contiguous):
+            raise TypeError("dst must be a contiguous numpy uint8 array")
+        size = ctypes.c_uint64()
+        dic = bytes(dictionary)
+        rc = self._lib.sz4_lz4(self._h, ctypes.c_void_p(src.ctypes.data), src.size, int(max_chain_length),
+                               dic if dic else None, len(dic), int(use_legacy_format),
+                               ctypes.c_void_p(dst.ctypes.data), dst.size, ctypes.byref(size))
+        self._check(rc, "sz4_lz4")
+        return size.value
+
     def lz4_stream(self, read, write, max_chain_length: int = MaxChainLength, dictionary: bytes = b"",
                    use_legacy_format: bool = False) -> None:
         """smallz4::lz4 over callbacks (sz4_lz4_stream): read(n) -> bytes (b"" at the end), write(bytes).
@@ -123,6 +139,10 @@ class Compressor:
     def set_stream_chunk(self, nbytes: int):
         """Input bytes per chunk of the stream paths (whole blocks; 0 = default 64 MiB)."""
         self._lib.sz4_set_stream_chunk(self._h, int(nbytes))
+
+    def set_batch_chunk(self, nbytes: int):
+        """Input bytes per internal piece of compress_blocks(_device) (whole blocks; 0 = default 128 MiB)."""
+        self._lib.sz4_set_batch_chunk(self._h, int(nbytes))
 
     # -- data-parallel entry point --------------------------------------------------------------
     def compress_blocks_device(self, d_in: int, n: int, d_out: int, out_cap: int, block_size: int = 65536,

@@ -39,6 +39,7 @@ SIGNATURES = {
     "sz4_lz4_bound": (_u64, [_u64, _i32]),
     "sz4_lz4_stream": (_i32, [_vp, GET_BYTES, SEND_BYTES, _u32, _vp, _u64, _i32, _vp]),
     "sz4_set_stream_chunk": (None, [_vp, _u64]),
+    "sz4_set_batch_chunk": (None, [_vp, _u64]),
     "sz4_unlz4_stream": (_i32, [_vp, GET_BYTE, SEND_OUT, _vp, _u64, _vp]),
     "sz4_last_stage_ms": (_i32, [_vp, ctypes.POINTER(ctypes.c_float), _i32]),
     "sz4_set_timing": (None, [_vp, _i32]),

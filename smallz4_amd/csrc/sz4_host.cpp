@@ -18,7 +18,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
-#include <thread>
+#include <new>
 #include <vector>
 
 #include "../../include/smallz4_amd.h"
@@ -131,13 +131,18 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
-  DevBuf chunkOut;             // stream path: one chunk's blocks
+  DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
+  DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
+  uint64_t batchChunk = 128ull << 20;  // sz4_compress_blocks_device: input bytes per internal pipeline run
+  bool batchChunked = false;           // the last sz4_compress_blocks_device call ran in several pieces
+  uint64_t streamPlanKey[5] = {~0ull, 0, 0, 0, 0};  // stream path: the chunk shape the current plan is for
   // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
   // (ghost slot nblocks of iv/ivCount, B.prev of the first block) and dictionary-mode state
   std::vector<Interval> ghostIv;
+  uint32_t ghostN = 0;
   bool ghost = false;
   uint32_t dictCont = 0, dictShift = 0, dictLow0 = 0;
   DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut, unSeq;  // decoder (sz4_unlz4*)
@@ -161,7 +166,9 @@ struct sz4_ctx {
   uint32_t planBS = 0;
   std::vector<uint32_t> hostBytes;
 
-  hipStream_t stream = nullptr;  // the stream path's own stream
+  hipStream_t stream = nullptr;  // the stream path's compute stream
+  hipStream_t upStream = nullptr, downStream = nullptr;  // its upload and download streams
+  hipEvent_t evUp[2] = {}, evDone[2] = {};  // per staging slot: upload complete, chunk computed
   bool pooled = false;           // handed out by sz4_acquire
   std::mutex* poolMu = nullptr;
   std::vector<sz4_ctx*>* poolIdle = nullptr;
@@ -170,8 +177,9 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &chunkOut, &lazySlots,
-            &unBlk, &unMeta, &unFlags, &unFrame, &unDict, &unOut, &unSeq};
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX,
+            &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
+            &unOut, &unSeq};
   }
 
   int fail(int code, const char* what, hipError_t e = hipSuccess)
@@ -305,12 +313,15 @@ void mark(sz4_ctx* c, int i, hipStream_t s)
   if (c->timing) hipEventRecord(c->ev[i], s);
 }
 
-// run the kernel pipeline over the planned blocks of c->staged; frame goes to `out`
-int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdrLen, bool endMark, uint8_t* out,
-                 uint64_t outCap, uint64_t* outSize, hipStream_t s)
+int pipeline_finish(sz4_ctx* c, const uint8_t* hdr, uint64_t hdrLen, bool endMark, uint8_t* out, uint64_t outCap,
+                    uint64_t* outSize, hipStream_t s);
+
+// run the kernel pipeline over the planned blocks of the staged input `in`; frame goes to `out`.
+// finish = false: return once every kernel is enqueued (pipeline_finish collects the result)
+int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t* hdr, uint64_t hdrLen, bool endMark,
+                 uint8_t* out, uint64_t outCap, uint64_t* outSize, hipStream_t s, bool finish = true)
 {
   const uint32_t nb = (uint32_t)c->hBlocks.size();
-  const uint8_t* in = c->staged.as<uint8_t>();
   c->lastChain = maxChain;
   hipError_t e;
   const void* at[4] = {c->blocks.p, c->segs.p, c->dpSegs.p, c->walkSegs.p};
@@ -325,11 +336,12 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   memcpy(c->uploadedAt, at, sizeof at);
   if ((e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
     return c->fail(SZ4_E_DEVICE, "upload plan", e);
-  // ghost slot nb: the previous chunk's last block (only its intervals are read, through B.prev)
-  const uint32_t ghostN = c->ghost ? (uint32_t)c->ghostIv.size() : 0u;
-  if ((ghostN && (e = hipMemcpyAsync(c->iv.as<Interval>() + (uint64_t)nb * kMaxIv, c->ghostIv.data(),
-                                     ghostN * sizeof(Interval), hipMemcpyHostToDevice, s))) ||
-      (e = hipMemcpyAsync(c->ivCount.as<uint32_t>() + nb, &ghostN, 4, hipMemcpyHostToDevice, s)))
+  // ghost slot nb: the previous chunk's last block (only its intervals are read, through B.prev).  The
+  // sources of these asynchronous copies live in the context: the stream path returns before they run
+  c->ghostN = c->ghost ? (uint32_t)c->ghostIv.size() : 0u;
+  if ((c->ghostN && (e = hipMemcpyAsync(c->iv.as<Interval>() + (uint64_t)nb * kMaxIv, c->ghostIv.data(),
+                                        c->ghostN * sizeof(Interval), hipMemcpyHostToDevice, s))) ||
+      (e = hipMemcpyAsync(c->ivCount.as<uint32_t>() + nb, &c->ghostN, 4, hipMemcpyHostToDevice, s)))
     return c->fail(SZ4_E_DEVICE, "upload intervals", e);
   const uint32_t ns = (uint32_t)c->hSegs.size();
   Block* dB = c->blocks.as<Block>();
@@ -414,7 +426,17 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
               c->status.as<int>(), s);
   mark(c, 6, s);
   if ((e = hipGetLastError())) return c->fail(SZ4_E_DEVICE, "kernel launch", e);
+  c->lastBlocks = nb;
+  if (!finish) return SZ4_OK;
+  return pipeline_finish(c, hdr, hdrLen, endMark, out, outCap, outSize, s);
+}
 
+// the frame size and device status of the pipeline enqueued last on s; header and end mark around it
+int pipeline_finish(sz4_ctx* c, const uint8_t* hdr, uint64_t hdrLen, bool endMark, uint8_t* out, uint64_t outCap,
+                    uint64_t* outSize, hipStream_t s)
+{
+  const uint32_t nb = (uint32_t)c->hBlocks.size();
+  hipError_t e;
   uint64_t total = 0;
   int status = 0;
   if ((e = hipMemcpyAsync(&total, c->offsets.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost, s)) ||
@@ -429,7 +451,6 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* hdr, uint64_t hdr
   if ((e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "finish", e);
   if (c->timing)
     for (int i = 0; i < kStages; i++) hipEventElapsedTime(&c->stageMs[i], c->ev[i], c->ev[i + 1]);
-  c->lastBlocks = nb;
   *outSize = size;
   return SZ4_OK;
 }
@@ -511,9 +532,10 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
 // from its predecessor -- the lookback cut (smallz4.h:614-624) and the positions the same-letter
 // shortcut left out of the chains -- comes along as the previous block's final intervals in the
 // ghost slot; dictionary mode carries the reference's hash table and chains.  The device footprint
-// is fixed by the chunk size, whatever the input length.  While the GPU compresses chunk i on a
-// worker thread, the caller's thread hands chunk i-1's blocks to sendBytes and pulls chunk i+1
-// through getBytes (both callbacks always run on the caller's thread).
+// is fixed by the chunk size, whatever the input length.  Three streams overlap the chunks: while the
+// compute stream runs chunk k+1, chunk k comes down on the download stream and goes to sendBytes, and
+// chunk k+2 is pulled through getBytes and goes up on the upload stream (two staging and two output
+// slots).  Both callbacks run on the caller's thread.
 constexpr uint64_t kCarryMax = 2 * 65536;
 
 struct MemSource {
@@ -539,94 +561,6 @@ void mem_send(const void* data, size_t n, void* user)
   m->n += n;
 }
 
-struct ChunkJob {
-  const uint8_t* host;  // pinned: the chunk's new bytes
-  uint64_t pre, n;      // carried bytes already staged, new bytes
-  bool first;           // the stream's first chunk
-  bool more;            // another chunk follows: prepare the carry
-  uint8_t* out;         // pinned: the chunk's blocks
-  uint64_t outSize;
-  uint64_t nextPre;
-  int rc;
-};
-
-// compresses one chunk (worker thread); on success the carry for the next chunk is in place
-int compress_chunk(sz4_ctx* c, uint32_t maxChain, int legacy, bool dictMode, ChunkJob& j)
-{
-  DeviceGuard guard(c->device);
-  hipStream_t s = c->stream;
-  const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
-  c->hBlocks.clear();
-  for (uint64_t st = 0; st < j.n; st += bs) {
-    Block B{};
-    B.start = j.pre + st;
-    B.end = j.pre + std::min(st + bs, j.n);
-    if (legacy || (st == 0 && j.first)) {
-      B.low = B.start;
-      B.cut = kNone;
-      B.prev = kNoBlock;
-    } else {
-      B.low = B.start - kWindow;
-      B.cut = B.start - kTailNoMatch;  // re-inserted by the lookback of the next block
-      B.prev = st == 0 ? kNoBlock - 1 : (uint32_t)c->hBlocks.size() - 1;  // first: the ghost slot, below
-    }
-    B.flags = legacy ? kBlkLegacy : 0;
-    c->hBlocks.push_back(B);
-  }
-  const uint32_t nb = (uint32_t)c->hBlocks.size();
-  if (c->hBlocks[0].prev == kNoBlock - 1) c->hBlocks[0].prev = nb;
-  c->ghost = !legacy && !j.first && !dictMode;
-  finish_plan(c);
-  c->planN = ~0ull;  // invalidate the independent-block plan cache
-  if (int r = reserve_all(c, j.pre + j.n + kPad)) return r;
-  hipError_t e;
-  const uint64_t cap = sz4_lz4_bound(j.n, legacy);
-  if ((e = c->chunkOut.reserve(cap))) return c->fail(SZ4_E_NOMEM, "chunk output", e);
-  uint8_t* staged = c->staged.as<uint8_t>();
-  if ((e = hipMemcpyAsync(staged + j.pre, j.host, j.n, hipMemcpyHostToDevice, s)) ||
-      (e = hipMemsetAsync(staged + j.pre + j.n, 0, kPad, s)))
-    return c->fail(SZ4_E_DEVICE, "upload", e);
-  uint64_t size = 0;
-  if (int r = run_pipeline(c, maxChain, nullptr, 0, false, c->chunkOut.as<uint8_t>(), cap, &size, s)) return r;
-  if ((e = hipMemcpyAsync(j.out, c->chunkOut.p, size, hipMemcpyDeviceToHost, s))) return c->fail(SZ4_E_DEVICE, "download", e);
-  j.outSize = size;
-  if (j.more) {
-    // carry: the last (pre + n - shift) bytes, shift a multiple of 65536 so that dictionary mode's
-    // absolute chain slots (pos & 65535) stay put; at least 65536 bytes precede the next chunk
-    const uint64_t end = j.pre + j.n;
-    const uint64_t shift = (end - 65536) / 65536 * 65536;
-    j.nextPre = end - shift;
-    if (!legacy && !dictMode) {
-      // the last block's final shortcut intervals become the next chunk's ghost slot
-      uint32_t cnt = 0;
-      if ((e = hipMemcpyAsync(&cnt, c->ivCount.as<uint32_t>() + (nb - 1), 4, hipMemcpyDeviceToHost, s)) ||
-          (e = hipStreamSynchronize(s)))
-        return c->fail(SZ4_E_DEVICE, "intervals", e);
-      std::vector<Interval> iv(cnt);
-      if (cnt && ((e = hipMemcpyAsync(iv.data(), c->iv.as<Interval>() + (uint64_t)(nb - 1) * kMaxIv, cnt * sizeof(Interval),
-                                      hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))))
-        return c->fail(SZ4_E_DEVICE, "intervals", e);
-      c->ghostIv.clear();
-      for (Interval x : iv) {
-        if (x.hi <= shift) continue;
-        x.lo = std::max(x.lo, shift) - shift;
-        x.hi -= shift;
-        x.a = x.a >= shift ? x.a - shift : 0;
-        c->ghostIv.push_back(x);
-      }
-    }
-    if (dictMode) {
-      c->dictCont = legacy ? 0u : 1u;
-      c->dictShift = (uint32_t)shift;
-      c->dictLow0 = (uint32_t)(j.nextPre - kWindow);
-    }
-    // the source [shift, end) and the destination [0, end - shift) do not overlap: end - shift <= 2 * 65536 <= shift
-    if ((e = hipMemcpyAsync(staged, staged + shift, j.nextPre, hipMemcpyDeviceToDevice, s))) return c->fail(SZ4_E_DEVICE, "carry", e);
-  }
-  if ((e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "chunk", e);
-  return SZ4_OK;
-}
-
 // the reference's output call pattern for a run of blocks: four 1-byte calls for the size word, then
 // the payload, also when it is empty (smallz4.h:770-780)
 void send_blocks(const uint8_t* f, uint64_t n, sz4_send_bytes send, void* user)
@@ -643,26 +577,100 @@ void send_blocks(const uint8_t* f, uint64_t n, sz4_send_bytes send, void* user)
   }
 }
 
-// reads up to `want` bytes through getBytes, 64 KiB per call (the reference's BufferSize); *eof is
-// set once getBytes has returned 0
-uint64_t pull(sz4_get_bytes get, void* user, uint8_t* dst, uint64_t want, bool* eof)
+// grows pinned buffer b to at least `bytes`, keeping its first `keep` bytes
+hipError_t grow_pinned(HostBuf& b, uint64_t bytes, uint64_t keep)
+{
+  if (bytes <= b.cap) return hipSuccess;
+  void* p = nullptr;
+  hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return e;
+  if (keep && b.p) memcpy(p, b.p, keep);
+  if (b.p) hipHostFree(b.p);
+  b.p = p;
+  b.cap = bytes;
+  return hipSuccess;
+}
+
+// reads up to `want` bytes through getBytes, 64 KiB per call (the reference's BufferSize), into pinned
+// buffer b, which grows as it fills (a small input pins little); *eof is set once getBytes returns 0.
+// A getBytes that returns more than it was asked for is an error (*bad)
+uint64_t pull(HostBuf& b, sz4_get_bytes get, void* user, uint64_t want, bool* eof, hipError_t* err, bool* bad)
 {
   uint64_t got = 0;
   while (got < want && !*eof) {
-    const size_t k = get(dst + got, (size_t)std::min<uint64_t>(65536, want - got), user);
+    if (got == b.cap && (*err = grow_pinned(b, std::min<uint64_t>(want, std::max<uint64_t>(4 * b.cap, 1u << 20)), got)))
+      return got;
+    const uint64_t ask = std::min<uint64_t>(65536, std::min<uint64_t>(want, b.cap) - got);
+    const size_t k = get(b.as<uint8_t>() + got, (size_t)ask, user);
+    if (k > ask) {
+      *bad = true;
+      *eof = true;
+      return got;
+    }
     if (k == 0) *eof = true;
     got += k;
   }
   return got;
 }
 
-int stream_compress(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t maxChain, const uint8_t* dict,
-                    uint64_t dictLen, int legacy, void* user, void* sinkUser = nullptr)
+// one chunk of the stream: [pre carried bytes | n new bytes] in stagedS[slot]
+struct StreamChunk {
+  uint64_t pre = 0, n = 0;
+  bool first = false;
+  uint64_t shift() const { return (pre + n - 65536) / 65536 * 65536; }  // carry: [shift, pre + n) moves to 0
+  uint64_t nextPre() const { return pre + n - shift(); }
+};
+
+// the block plan of a chunk (smallz4.h:572-585: 4 MiB blocks seeing the previous 64 KiB, or 8 MiB
+// independent legacy blocks); cached: equal-shaped chunks reuse the plan and its device copy
+void plan_chunk(sz4_ctx* c, const StreamChunk& ch, int legacy, bool dictMode)
 {
-  void* out = sinkUser ? sinkUser : user;
+  const uint64_t key[5] = {ch.pre, ch.n, ch.first ? 1ull : 0ull, (uint64_t)legacy, dictMode ? 1ull : 0ull};
+  if (memcmp(key, c->streamPlanKey, sizeof key) == 0) return;
+  memcpy(c->streamPlanKey, key, sizeof key);
+  const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
+  c->hBlocks.clear();
+  for (uint64_t st = 0; st < ch.n; st += bs) {
+    Block B{};
+    B.start = ch.pre + st;
+    B.end = ch.pre + std::min(st + bs, ch.n);
+    if (legacy || (st == 0 && ch.first)) {
+      B.low = B.start;
+      B.cut = kNone;
+      B.prev = kNoBlock;
+    } else {
+      B.low = B.start - kWindow;
+      B.cut = B.start - kTailNoMatch;  // re-inserted by the lookback of the next block
+      B.prev = st == 0 ? kNoBlock - 1 : (uint32_t)c->hBlocks.size() - 1;  // first: the ghost slot, below
+    }
+    B.flags = legacy ? kBlkLegacy : 0;
+    c->hBlocks.push_back(B);
+  }
+  const uint32_t nb = (uint32_t)c->hBlocks.size();
+  if (nb && c->hBlocks[0].prev == kNoBlock - 1) c->hBlocks[0].prev = nb;
+  finish_plan(c);
+  c->planN = ~0ull;  // invalidate the independent-block plan cache
+}
+
+// drains the stream path's streams before an early return (nothing may still run on its buffers)
+struct StreamDrain {
+  sz4_ctx* c;
+  ~StreamDrain()
+  {
+    for (hipStream_t x : {c->upStream, c->stream, c->downStream})
+      if (x) hipStreamSynchronize(x);
+  }
+};
+
+int stream_compress_body(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t maxChain, const uint8_t* dict,
+                         uint64_t dictLen, int legacy, void* user, void* out)
+{
   hipError_t e;
-  if (!c->stream && (e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking)))
-    return c->fail(SZ4_E_DEVICE, "stream", e);
+  for (hipStream_t* x : {&c->stream, &c->upStream, &c->downStream})
+    if (!*x && (e = hipStreamCreateWithFlags(x, hipStreamNonBlocking))) return c->fail(SZ4_E_DEVICE, "stream", e);
+  for (int k = 0; k < 2; k++)
+    for (hipEvent_t* x : {&c->evUp[k], &c->evDone[k]})
+      if (!*x && (e = hipEventCreateWithFlags(x, hipEventDisableTiming))) return c->fail(SZ4_E_DEVICE, "event", e);
   const uint64_t bs = legacy ? kBlockMaxLegacy : kBlockMax;
   const uint64_t chunk = std::max<uint64_t>(bs, c->streamChunk / bs * bs);
   const bool dictMode = dictLen != 0;
@@ -670,55 +678,170 @@ int stream_compress(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t
   const uint8_t hm[7] = {0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF};
   const uint8_t hl[4] = {0x02, 0x21, 0x4C, 0x18};
   send(legacy ? hl : hm, legacy ? 4 : 7, out);
-  if ((e = c->hostIn[0].reserve(chunk)) || (e = c->hostIn[1].reserve(chunk)) ||
-      (e = c->hostOut[0].reserve(sz4_lz4_bound(chunk, legacy))) || (e = c->hostOut[1].reserve(sz4_lz4_bound(chunk, legacy))))
-    return c->fail(SZ4_E_NOMEM, "pinned host buffers", e);
-  // fixed device footprint: the staged buffer is sized once for the largest chunk (the carry lives in it)
-  if ((e = c->staged.reserve(kCarryMax + chunk + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
-  bool eof = false;
-  uint64_t n = pull(get, user, c->hostIn[0].as<uint8_t>(), chunk, &eof);
+  StreamDrain drain{c};
+  bool eof = false, bad = false;
+  hipError_t he = hipSuccess;
+  StreamChunk ch[2];
+  ch[0].n = pull(c->hostIn[0], get, user, chunk, &eof, &he, &bad);
+  if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
+  if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
   // dictionary: the staged stream starts with the reference's data buffer, a 65535-byte prefix (the
   // dictionary's last bytes, zero-padded in front) (smallz4.h:554-571)
-  uint64_t pre = 0;
   c->dictBack = dictMode ? (int64_t)std::min<uint64_t>(dictLen, kWindow) : -1;
   c->dictLegacy = legacy;
   c->dictCont = 0;
   c->ghost = false;
-  if (dictMode && n) {
-    pre = kWindow;
-    std::vector<uint8_t> prefix(pre, 0);
-    const uint64_t k = std::min<uint64_t>(dictLen, pre);
-    memcpy(prefix.data() + pre - k, dict + dictLen - k, k);
-    if ((e = hipMemcpy(c->staged.p, prefix.data(), pre, hipMemcpyHostToDevice))) return c->fail(SZ4_E_DEVICE, "upload", e);
+  ch[0].pre = dictMode && ch[0].n ? kWindow : 0;
+  ch[0].first = true;
+  if (ch[0].n) {
+    // device buffers fixed by the chunk size (by the input when it is shorter than a chunk); the
+    // scratch is sized once for the steady-state chunk shape, so no buffer moves mid-stream
+    const uint64_t span = eof ? ch[0].n : chunk;
+    const uint64_t stage = (eof ? ch[0].pre : kCarryMax) + span + kPad;
+    if ((e = c->stagedS[0].reserve(stage)) || (!eof && (e = c->stagedS[1].reserve(stage))) ||
+        (e = c->chunkOut[0].reserve(sz4_lz4_bound(span, legacy))) ||
+        (!eof && (e = c->chunkOut[1].reserve(sz4_lz4_bound(span, legacy)))))
+      return c->fail(SZ4_E_NOMEM, "stream staging", e);
+    StreamChunk worst;
+    worst.pre = eof ? ch[0].pre : kCarryMax - 1;
+    worst.n = span;
+    worst.first = eof;
+    plan_chunk(c, worst, legacy, dictMode);
+    if (int r = reserve_all(c, worst.pre + worst.n + kPad)) return r;
   }
-  ChunkJob prevJob{};
-  bool havePrev = false;
-  for (uint32_t i = 0; n; i++) {
-    ChunkJob j{};
-    j.host = c->hostIn[i & 1].as<uint8_t>();
-    j.pre = pre;
-    j.n = n;
-    j.first = i == 0;
-    j.more = n == chunk && !eof;
-    j.out = c->hostOut[i & 1].as<uint8_t>();
-    j.rc = SZ4_OK;
-    std::thread worker([&]() { j.rc = compress_chunk(c, maxChain, legacy, dictMode, j); });
-    // meanwhile, on the caller's thread: the previous chunk's blocks out, the next chunk's bytes in
-    if (havePrev) send_blocks(prevJob.out, prevJob.outSize, send, out);
-    const uint64_t next = j.more ? pull(get, user, c->hostIn[(i + 1) & 1].as<uint8_t>(), chunk, &eof) : 0;
-    worker.join();
-    if (j.rc != SZ4_OK) return j.rc;
-    prevJob = j;
-    havePrev = true;
-    pre = j.nextPre;
-    n = next;
+  if (dictMode && ch[0].n) {
+    std::vector<uint8_t> prefix(kWindow, 0);
+    const uint64_t k = std::min<uint64_t>(dictLen, kWindow);
+    memcpy(prefix.data() + kWindow - k, dict + dictLen - k, k);
+    if ((e = hipMemcpy(c->stagedS[0].p, prefix.data(), kWindow, hipMemcpyHostToDevice)))
+      return c->fail(SZ4_E_DEVICE, "upload", e);
   }
-  if (havePrev) send_blocks(prevJob.out, prevJob.outSize, send, out);
+  // chunk k -> slot k & 1: upload on the copy stream (after chunk k-2 let go of the slot), with the
+  // previous chunk's carried bytes in front
+  auto upload = [&](uint32_t k) -> int {
+    const uint32_t sl = k & 1;
+    const StreamChunk& x = ch[sl];
+    uint8_t* dst = c->stagedS[sl].as<uint8_t>();
+    if (k >= 2 && (e = hipStreamWaitEvent(c->upStream, c->evDone[sl], 0))) return c->fail(SZ4_E_DEVICE, "upload", e);
+    if ((e = hipMemcpyAsync(dst + x.pre, c->hostIn[sl].p, x.n, hipMemcpyHostToDevice, c->upStream)) ||
+        (k >= 1 && (e = hipMemcpyAsync(dst, c->stagedS[sl ^ 1].as<uint8_t>() + ch[sl ^ 1].shift(), x.pre,
+                                       hipMemcpyDeviceToDevice, c->upStream))) ||
+        (e = hipMemsetAsync(dst + x.pre + x.n, 0, kPad, c->upStream)) || (e = hipEventRecord(c->evUp[sl], c->upStream)))
+      return c->fail(SZ4_E_DEVICE, "upload", e);
+    return SZ4_OK;
+  };
+  // enqueue chunk k's pipeline on the compute stream (returns with the kernels in flight)
+  auto compute = [&](uint32_t k) -> int {
+    const uint32_t sl = k & 1;
+    const StreamChunk& x = ch[sl];
+    c->ghost = !legacy && !x.first && !dictMode;
+    plan_chunk(c, x, legacy, dictMode);
+    if (int r = reserve_all(c, x.pre + x.n + kPad)) return r;
+    if ((e = hipStreamWaitEvent(c->stream, c->evUp[sl], 0))) return c->fail(SZ4_E_DEVICE, "chunk", e);
+    uint64_t unused = 0;
+    if (int r = run_pipeline(c, maxChain, c->stagedS[sl].as<uint8_t>(), nullptr, 0, false, c->chunkOut[sl].as<uint8_t>(),
+                             c->chunkOut[sl].cap, &unused, c->stream, false))
+      return r;
+    if ((e = hipEventRecord(c->evDone[sl], c->stream))) return c->fail(SZ4_E_DEVICE, "chunk", e);
+    return SZ4_OK;
+  };
+  // chunk k's frame size; the state its successor takes: the last block's final shortcut intervals
+  // (the ghost slot) and dictionary mode's table position
+  auto finish = [&](uint32_t k, uint64_t* size) -> int {
+    const uint32_t sl = k & 1;
+    const StreamChunk& x = ch[sl];
+    if (int r = pipeline_finish(c, nullptr, 0, false, c->chunkOut[sl].as<uint8_t>(), c->chunkOut[sl].cap, size, c->stream))
+      return r;
+    const uint64_t shift = x.shift();
+    const uint32_t nb = (uint32_t)c->hBlocks.size();
+    if (!legacy && !dictMode) {
+      uint32_t cnt = 0;
+      if ((e = hipMemcpyAsync(&cnt, c->ivCount.as<uint32_t>() + (nb - 1), 4, hipMemcpyDeviceToHost, c->stream)) ||
+          (e = hipStreamSynchronize(c->stream)))
+        return c->fail(SZ4_E_DEVICE, "intervals", e);
+      std::vector<Interval> iv(cnt);
+      if (cnt && ((e = hipMemcpyAsync(iv.data(), c->iv.as<Interval>() + (uint64_t)(nb - 1) * kMaxIv, cnt * sizeof(Interval),
+                                      hipMemcpyDeviceToHost, c->stream)) || (e = hipStreamSynchronize(c->stream))))
+        return c->fail(SZ4_E_DEVICE, "intervals", e);
+      c->ghostIv.clear();
+      for (Interval y : iv) {
+        if (y.hi <= shift) continue;
+        y.lo = std::max(y.lo, shift) - shift;
+        y.hi -= shift;
+        y.a = y.a >= shift ? y.a - shift : 0;
+        c->ghostIv.push_back(y);
+      }
+    }
+    if (dictMode) {
+      c->dictCont = legacy ? 0u : 1u;
+      c->dictShift = (uint32_t)shift;
+      c->dictLow0 = (uint32_t)(x.nextPre() - kWindow);
+    }
+    return SZ4_OK;
+  };
+  // the next chunk's bytes: [previous chunk's carry | new bytes]
+  auto next_chunk = [&](uint32_t k) -> bool {
+    const uint32_t sl = k & 1;
+    if (eof) return false;
+    if (k >= 2 && (e = hipEventSynchronize(c->evUp[sl]))) {  // the pinned buffer's previous upload
+      c->fail(SZ4_E_DEVICE, "upload", e);
+      return false;
+    }
+    ch[sl].n = pull(c->hostIn[sl], get, user, chunk, &eof, &he, &bad);
+    ch[sl].pre = ch[sl ^ 1].nextPre();
+    ch[sl].first = false;
+    return ch[sl].n != 0 && !he && !bad;
+  };
+  if (!ch[0].n) {
+    if (!legacy) {
+      static const uint8_t zero[4] = {0, 0, 0, 0};
+      send(zero, 4, out);  // end mark (smallz4.h:807-812)
+    }
+    return SZ4_OK;
+  }
+  if (int r = upload(0)) return r;
+  if (int r = compute(0)) return r;
+  bool have = next_chunk(1);
+  if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
+  if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
+  if (have)
+    if (int r = upload(1)) return r;
+  for (uint32_t k = 0;; k++) {
+    const uint32_t sl = k & 1;
+    uint64_t size = 0;
+    if (int r = finish(k, &size)) return r;
+    if (have)
+      if (int r = compute(k + 1)) return r;  // the GPU goes on with chunk k+1 ...
+    // ... while chunk k comes down and goes out, and chunk k+2 is read and goes up
+    if ((e = grow_pinned(c->hostOut[sl], std::max<uint64_t>(size, 1), 0))) return c->fail(SZ4_E_NOMEM, "pinned host buffers", e);
+    if ((e = hipMemcpyAsync(c->hostOut[sl].p, c->chunkOut[sl].p, size, hipMemcpyDeviceToHost, c->downStream)) ||
+        (e = hipStreamSynchronize(c->downStream)))
+      return c->fail(SZ4_E_DEVICE, "download", e);
+    send_blocks(c->hostOut[sl].as<uint8_t>(), size, send, out);
+    if (!have) break;
+    have = next_chunk(k + 2);
+    if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
+    if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
+    if (have)
+      if (int r = upload(k + 2)) return r;
+  }
   if (!legacy) {
     static const uint8_t zero[4] = {0, 0, 0, 0};
     send(zero, 4, out);  // end mark (smallz4.h:807-812)
   }
   return SZ4_OK;
+}
+
+// smallz4::lz4 over the callbacks.  A callback's exception (a C++ caller's sendBytes may throw) leaves
+// through here after the streams have drained; an allocation failure becomes SZ4_E_NOMEM
+int stream_compress(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t maxChain, const uint8_t* dict,
+                    uint64_t dictLen, int legacy, void* user, void* sinkUser = nullptr)
+{
+  try {
+    return stream_compress_body(c, get, send, maxChain, dict, dictLen, legacy, user, sinkUser ? sinkUser : user);
+  } catch (const std::bad_alloc&) {
+    return c->fail(SZ4_E_NOMEM, "host allocation");
+  }
 }
 
 // ---- decoder stream path: unlz4_userPtr over GET_BYTE / SEND_BYTES in bounded memory -----------
@@ -746,6 +869,8 @@ uint64_t legacy_block_length(const uint8_t* p, uint64_t len)
   }
   return w;
 }
+
+constexpr uint32_t kMaxFrameBlock = (uint32_t)(kBlockMaxLegacy + kBlockMaxLegacy / 255 + 16);  // LZ4 compress bound
 
 int stream_decompress(sz4_ctx* c, sz4_get_byte get, sz4_send_out send, const uint8_t* dict, uint64_t dictLen, void* user)
 {
@@ -811,6 +936,9 @@ int stream_decompress(sz4_ctx* c, sz4_get_byte get, sz4_send_out send, const uin
     if (modern) word &= 0x7FFFFFFFu;
     if (word == 0) break;
     if (legacy && (word & 0x80000000u)) return c->fail(SZ4_E_CORRUPT, "invalid or truncated LZ4 frame");
+    // no LZ4 block is larger than a legacy 8 MiB block's worst case: a larger size word is corrupt
+    // (the reference would read on until its input ends; this decoder must not reserve gigabytes first)
+    if (word > kMaxFrameBlock) return c->fail(SZ4_E_CORRUPT, "block size word larger than any LZ4 block");
     const uint64_t at = frame.size();
     frame.resize(at + 4 + word);
     const uint32_t tagged = word | (packed ? 0u : 0x80000000u);
@@ -860,7 +988,11 @@ void sz4_destroy(sz4_ctx* c)
   DeviceGuard guard(c->device);
   for (DevBuf* b : c->all_buffers()) b->release();
   for (HostBuf* b : {&c->hostIn[0], &c->hostIn[1], &c->hostOut[0], &c->hostOut[1]}) b->release();
-  if (c->stream) hipStreamDestroy(c->stream);
+  for (hipStream_t x : {c->stream, c->upStream, c->downStream})
+    if (x) hipStreamDestroy(x);
+  for (int k = 0; k < 2; k++)
+    for (hipEvent_t x : {c->evUp[k], c->evDone[k]})
+      if (x) hipEventDestroy(x);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   delete c;
@@ -921,33 +1053,10 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   // the kernels write the frame in place: refuse a buffer that could be overrun
   if (out_cap < sz4_bound(n, block_size)) return c->fail(SZ4_E_CAPACITY, "out_cap < sz4_bound(n, block_size)");
   DeviceGuard guard(c->device);
+  try {
   c->ghost = false;
   hipStream_t s = (hipStream_t)stream;
   c->dictBack = -1;
-  if (c->planN != n || c->planBS != block_size) {
-    c->hBlocks.clear();
-    for (uint64_t st = 0; st < n; st += block_size) {
-      Block B{};
-      B.start = st;
-      B.end = std::min<uint64_t>(st + block_size, n);
-      B.low = st;
-      B.cut = kNone;
-      B.prev = kNoBlock;
-      B.flags = 0;
-      c->hBlocks.push_back(B);
-    }
-    finish_plan(c);
-    c->planN = n;
-    c->planBS = block_size;
-  }
-  if (int r = reserve_all(c, n + kPad)) return r;
-  hipError_t e;
-  if ((e = c->staged.reserve(n + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
-  // private padded copy: kernels read 4-byte windows that may run past the caller's buffer
-  if (n && (e = hipMemcpyAsync(c->staged.p, d_in, n, hipMemcpyDeviceToDevice, s)))
-    return c->fail(SZ4_E_DEVICE, "stage input", e);
-  if ((e = hipMemsetAsync(c->staged.as<uint8_t>() + n, 0, kPad, s))) return c->fail(SZ4_E_DEVICE, "stage pad", e);
-
   uint8_t hdr[8];
   uint64_t hl = 0;
   bool endMark = true;
@@ -965,6 +1074,7 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   } else {
     endMark = false;
   }
+  c->batchChunked = false;
   if (n == 0) {
     if (out_cap < hl + (endMark ? 4 : 0)) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
     if (hl) hipMemcpyAsync(d_out, hdr, hl, hipMemcpyHostToDevice, s);
@@ -974,12 +1084,72 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
     *out_size = hl + (endMark ? 4 : 0);
     return SZ4_OK;
   }
-  return run_pipeline(c, max_chain, hdr, hl, endMark, (uint8_t*)d_out, out_cap, out_size, s);
+  // bounded memory: whole blocks in pieces of at most batchChunk input bytes, one pipeline run each
+  // (the scratch is ~60-75 bytes per input byte), written one after the other into d_out
+  const uint64_t piece = std::max<uint64_t>(block_size, c->batchChunk / block_size * block_size);
+  float stageSum[kStages] = {};
+  uint64_t pos = 0;
+  if (n > piece) c->hostBytes.clear();
+  for (uint64_t off = 0; off < n; off += piece) {
+    const uint64_t len = std::min(piece, n - off);
+    const bool firstPiece = off == 0, lastPiece = off + len == n;
+    if (c->planN != len || c->planBS != block_size) {
+      c->hBlocks.clear();
+      for (uint64_t st = 0; st < len; st += block_size) {
+        Block B{};
+        B.start = st;
+        B.end = std::min<uint64_t>(st + block_size, len);
+        B.low = st;
+        B.cut = kNone;
+        B.prev = kNoBlock;
+        B.flags = 0;
+        c->hBlocks.push_back(B);
+      }
+      finish_plan(c);
+      c->planN = len;
+      c->planBS = block_size;
+      c->streamPlanKey[0] = ~0ull;  // invalidate the stream path's plan cache
+    }
+    if (int r = reserve_all(c, len + kPad)) return r;
+    hipError_t e;
+    if ((e = c->staged.reserve(len + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
+    // private padded copy: kernels read 4-byte windows that may run past the caller's buffer
+    if ((e = hipMemcpyAsync(c->staged.p, (const uint8_t*)d_in + off, len, hipMemcpyDeviceToDevice, s)))
+      return c->fail(SZ4_E_DEVICE, "stage input", e);
+    if ((e = hipMemsetAsync(c->staged.as<uint8_t>() + len, 0, kPad, s))) return c->fail(SZ4_E_DEVICE, "stage pad", e);
+    uint64_t size = 0;
+    if (int r = run_pipeline(c, max_chain, c->staged.as<uint8_t>(), hdr, firstPiece ? hl : 0, lastPiece && endMark,
+                             (uint8_t*)d_out + pos, out_cap - pos, &size, s))
+      return r;
+    pos += size;
+    for (int i = 0; i < kStages; i++) stageSum[i] += c->stageMs[i];
+    if (n > piece) {
+      // every piece's block sizes, for sz4_last_block_sizes
+      const uint32_t nb = (uint32_t)c->hBlocks.size();
+      const size_t at = c->hostBytes.size();
+      c->hostBytes.resize(at + nb);
+      if ((e = hipMemcpy(c->hostBytes.data() + at, c->blockBytes.p, nb * 4, hipMemcpyDeviceToHost)))
+        return c->fail(SZ4_E_DEVICE, "block sizes", e);
+    }
+  }
+  c->batchChunked = n > piece;
+  if (c->timing)
+    for (int i = 0; i < kStages; i++) c->stageMs[i] = stageSum[i];
+  *out_size = pos;
+  return SZ4_OK;
+  } catch (const std::bad_alloc&) {
+    return c->fail(SZ4_E_NOMEM, "host allocation");
+  }
 }
 
 int64_t sz4_last_block_sizes(sz4_ctx* c, uint32_t* sizes, uint64_t max_blocks)
 {
   if (!c || !sizes) return SZ4_E_ARG;
+  if (c->batchChunked) {
+    const uint64_t nb = std::min<uint64_t>(c->hostBytes.size(), max_blocks);
+    for (uint64_t i = 0; i < nb; i++) sizes[i] = c->hostBytes[i] & 0x7FFFFFFFu;
+    return (int64_t)nb;
+  }
   const uint64_t nb = std::min<uint64_t>(c->lastBlocks, max_blocks);
   if (nb && hipMemcpy(sizes, c->blockBytes.p, nb * 4, hipMemcpyDeviceToHost) != hipSuccess) return SZ4_E_DEVICE;
   for (uint64_t i = 0; i < nb; i++) sizes[i] &= 0x7FFFFFFFu;
@@ -1016,6 +1186,11 @@ int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const vo
 void sz4_set_stream_chunk(sz4_ctx* c, uint64_t bytes)
 {
   if (c) c->streamChunk = bytes ? bytes : (64ull << 20);
+}
+
+void sz4_set_batch_chunk(sz4_ctx* c, uint64_t bytes)
+{
+  if (c) c->batchChunk = bytes ? bytes : (128ull << 20);
 }
 
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)
@@ -1101,7 +1276,11 @@ int sz4_unlz4_stream(sz4_ctx* c, sz4_get_byte get_byte, sz4_send_out send_bytes,
   if (!c || !get_byte || !send_bytes || (dict_len && !dict)) return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
   c->err.clear();
   DeviceGuard guard(c->device);
-  return stream_decompress(c, get_byte, send_bytes, (const uint8_t*)dict, dict_len, user);
+  try {
+    return stream_decompress(c, get_byte, send_bytes, (const uint8_t*)dict, dict_len, user);
+  } catch (const std::bad_alloc&) {
+    return c->fail(SZ4_E_NOMEM, "host allocation");
+  }
 }
 
 uint64_t sz4_device_bytes(sz4_ctx* c)

@@ -110,11 +110,16 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
 }
 
 // DPP row (16-lane) permutations
-#if SZ4_DIAG == 3
+#if SZ4_DIAG == 3 || SZ4_DIAG == 4
 __device__ uint64_t sz4_diag[1 << 20];
 extern "C" int sz4_diag_read(uint64_t* out, uint64_t n)
 {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(sz4_diag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int sz4_diag_clear()
+{
+  static uint64_t zero[64] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(sz4_diag), zero, sizeof zero, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
 }
 #endif
 
@@ -691,7 +696,9 @@ template <bool kLds>
 constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_big / k_find_long9
-constexpr uint32_t kBigRun = 256;     // the same for a run key (vvvv) in blocks k_find_big takes
+constexpr uint32_t kBigRun = 2048;    // the same for a run key (vvvv) in blocks k_find_big takes
+constexpr uint32_t kLpfMin = 256;     // ... and for any key of an LPF group (below)
+constexpr uint32_t kLpfProbe = 8;
 __device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
 constexpr uint32_t kFlagRmq = 1;   // longFlag: the block has matches of kRmqLen+ (other than same-letter runs)
@@ -712,6 +719,26 @@ __device__ __forceinline__ uint32_t slot_pos(const void* base, bool small, uint3
 __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32_t E, uint32_t s)
 {
   return small ? (uint32_t)reinterpret_cast<const uint16_t*>(base)[E + s] : reinterpret_cast<const uint32_t*>(base)[E + s];
+}
+
+// An LPF group (k_find_big): a key group whose first kLpfProbe members share
+// their preceding byte -- records, markup, tables: most candidates of a target then share its
+// preceding byte too and carry from p-1, so k_find_big's left-maximal search takes its targets from
+// kLpfMin candidates on.  A function of the group start and the text, so that k_find_sorted and
+// k_find_big agree on it.  predLo: positions at or below it have no known predecessor.
+template <class Src>
+__device__ __forceinline__ bool lpf_group(const void* compact, bool small, uint32_t gs, uint64_t w0, uint64_t predLo,
+                                          const Src& src)
+{
+  uint32_t c0 = 0;
+  for (uint32_t k = 0; k < kLpfProbe; k++) {
+    const uint64_t q = w0 + slot_pos(compact, small, gs + k);
+    if (q <= predLo) return false;
+    const uint32_t c = src.ld4(q - 1) & 0xFFu;
+    if (k == 0) c0 = c;
+    else if (c != c0) return false;
+  }
+  return true;
 }
 
 template <bool kLds>
@@ -839,8 +866,13 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     // -9, a target with more than kBigGroup candidates (runs, periodic data): left to k_find_long9,
     // which walks in text order and prunes with the previous target's result
     // (k_find_big takes blocks without a lookback cut or shortcut intervals; there run keys go from kBigRun on)
-    const bool lpfRun = B.cut == kNone && ivCount[S.block] == 0u && (B.prev == kNoBlock || ivCount[B.prev] == 0u);
-    const bool big = unlimited && cut == kNone && active && slot - gs > (lpfRun && run_key(me0) ? kBigRun : kBigGroup);
+    const bool lpfOk = B.cut == kNone && ivCount[S.block] == 0u && (B.prev == kNoBlock || ivCount[B.prev] == 0u);
+    // (a run group: its first member's key is a run key -- the group start decides, as in k_find_big)
+    const bool big = unlimited && cut == kNone && active &&
+                     (slot - gs > kBigGroup ||
+                      (lpfOk && slot - gs > kLpfMin &&
+                       ((slot - gs > kBigRun && run_key(src.ld4(S.w0 + slot_pos(compact, small, gs)))) ||
+                        lpf_group(compact, small, gs, S.w0, S.w0 > B.low ? S.w0 : B.low, src))));
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
@@ -2151,17 +2183,10 @@ __global__ __launch_bounds__(kFindThreads) void k_find_long9_hbm(SZ4_LONG9_ARGS)
 // Only blocks without a lookback cut or shortcut intervals (independent blocks): the identity needs
 // every candidate position to be a chain position.
 // ================================================================================================
-constexpr uint32_t kMaxBigGroups = 32;  // > 128 Ki window slots / kBigGroup, plus run-key groups
+constexpr uint32_t kMaxBigGroups = 256;  // big, run-key and LPF groups of one segment (> 128 Ki / 512)
 constexpr uint32_t kClsNone = 256;      // preceding byte class of a position without a chain predecessor
-// run-key groups (key vvvv, runs of one byte value) are binned by their run length R (bytes equal to v
-// from the position on, within the block): a candidate of the same R shares R bytes and the next one
-// decides; every other R gives min(R(p), R(c))
-constexpr uint32_t kRunCap = 256;                             // R = 4..255 exact, 256 = at least 256
-constexpr uint32_t kBinRun0 = kClsNone + 1;                   // bins 0..256: class of a non-run member
-constexpr uint32_t kBins = kBinRun0 + 2 * (kRunCap - 3);      // then per R: run interior, run start
-constexpr uint32_t kNoBin = 0xFFFFFFFFu;
-static_assert(kBins <= kFindThreads, "one bin per thread in the bin scan");
-
+constexpr uint32_t kBins = kClsNone + 1;
+constexpr uint32_t kAEnd = 256;         // run table: a run that reaches the block end has no next byte
 
 // exclusive prefix sums of v over the workgroup's threads (thread i: bin i); total in *tot
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* tot)
@@ -2189,21 +2214,37 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
                                                            uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
                                                            uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                            uint64_t matchBase, uint32_t* __restrict__ lm, uint64_t* __restrict__ segTail,
-                                                           uint32_t resolveOnly)
+                                                           uint32_t* __restrict__ runBkt, uint32_t resolveOnly)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_groups[2 * kMaxBigGroups];
-  __shared__ uint32_t s_ng, s_next;
-  __shared__ uint32_t s_cls[kBins + 1], s_tcls[kBins + 1];  // bin starts (candidates, targets)
+  __shared__ uint32_t s_ng, s_next, s_mixed, s_nRuns;
+  __shared__ uint32_t s_cls[kBins + 1], s_tcls[kBins + 1];  // bin starts (candidates, targets); run buckets
   __shared__ uint32_t s_cur[2][kBins];                      // counts, then scatter cursors
   __shared__ uint32_t s_wsum[kFindThreads / 64];
   __shared__ uint32_t s_hasHead[kFindThreads / 64], s_outValid[kFindThreads / 64];
   __shared__ uint64_t s_outKey[kFindThreads / 64];
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
-  if (!segLong[blockIdx.x] || B.cut != kNone || ivCount[S.block] != 0u || (B.prev != kNoBlock && ivCount[B.prev] != 0u))
-    return;  // uniform over the workgroup
+  if (B.cut != kNone || ivCount[S.block] != 0u || (B.prev != kNoBlock && ivCount[B.prev] != 0u))
+    return;  // uniform over the workgroup (the resolve launch returns here for every segment of the block)
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  if (!resolveOnly && tid == 0) {
+    // the state after this segment's last target for the next segment's resolve launch, as it stands
+    // when no target here is left to this kernel (no big group, or more than fit): the last target's
+    // own result when pass 1 finished it, else unknown.  Phase 3 below overwrites it.
+    const uint32_t nTg = (uint32_t)(S.s1 - S.s0);
+    const uint64_t idx = S.s1 - 1 - matchBase;
+    const uint32_t ml = mlen[idx], md = mdist[idx];
+    uint64_t t = 0;
+    if (ml != kLongMatch) {
+      const uint64_t e = (uint64_t)(nTg - 1) + ml;  // match end relative to s0
+      t = (1ull << 63) | (ml >= (uint32_t)kMinMatch && e > (uint64_t)nTg + kMinMatch - 1u
+                              ? ((e - nTg) << 16) | (0xFFFFu - md) : 0ull);
+    }
+    segTail[blockIdx.x] = t;
+  }
+  if (!segLong[blockIdx.x]) return;  // uniform
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
   const void* compact = compactAll + S.elemOff;
   const uint32_t E = (uint32_t)(S.s1 - S.w0);  // no intervals: every window position is a slot
@@ -2213,10 +2254,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   //    kBigGroup candidates, or kBigRun for a run key: the same predicate as k_find_sorted's)
   if (tid == 0) s_ng = 0;
   __syncthreads();
+  const uint64_t predLo0 = S.w0 > B.low ? S.w0 : B.low;
+  const Bytes<false> gsrc{in};
   for (uint32_t s = tid; s < E; s += kFindThreads) {
     const uint32_t g = slot_gs(compact, small, E, s);
-    if (s - g > kBigRun && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g) &&
-        (s - g > kBigGroup || run_key(gload4(in, S.w0 + slot_pos(compact, small, s))))) {
+    if (s - g > kLpfMin && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g) &&
+        (s - g > kBigGroup || (s - g > kBigRun && run_key(gload4(in, S.w0 + slot_pos(compact, small, g)))) ||
+         lpf_group(compact, small, g, S.w0, predLo0, gsrc))) {
       const uint32_t k = atomicAdd(&s_ng, 1u);
       if (k < kMaxBigGroups) {
         s_groups[2 * k] = g;
@@ -2247,44 +2291,244 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
   auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
-  // bin of a member: its class, or for a run key its run length R (capped at kRunCap, within the block)
-  // and whether it starts the run (its class is not the run's byte)
-  auto bin_of = [&](uint64_t q, uint32_t key) -> uint32_t {
-    const uint32_t c = cls_of(q);
-    if (!run_key(key)) return c;
-    const uint64_t left = B.end - q;
-    const uint32_t lim = left < kRunCap ? (uint32_t)left : kRunCap;
-    uint32_t r = 4;
-    while (r < lim) {
-      const uint32_t x = src.ld4(q + r) ^ key;
-      if (x) {
-        r += (uint32_t)__builtin_ctz(x) >> 3;
+  // the same predicate as k_find_sorted's `big` (key: the group's first member's; lpfG: an LPF group)
+  auto is_target = [&](uint32_t s, uint32_t ga, uint64_t q, uint32_t key, bool lpfG) {
+    return q >= S.s0 && (s - ga > kBigGroup || (run_key(key) && s - ga > kBigRun) || (lpfG && s - ga > kLpfMin));
+  };
+  // common prefix of the texts at x and y, at most `cap` bytes (both readable that far)
+  auto ext_len = [&](uint64_t x, uint64_t y, uint32_t cap) -> uint32_t {
+    uint32_t k = 0;
+    while (k < cap) {
+      const uint32_t d = src.ld4(x + k) ^ src.ld4(y + k);
+      if (d) {
+        k += (uint32_t)__builtin_ctz(d) >> 3;
         break;
       }
-      r += 4;
+      k += 4;
     }
-    r = r < lim ? r : lim;
-    return kBinRun0 + 2u * (r - 4u) + (c != (key & 0xFFu) ? 1u : 0u);
+    return k < cap ? k : cap;
   };
-  auto is_target = [&](uint32_t s, uint32_t ga, uint64_t q, uint32_t key) {
-    return q >= S.s0 && s - ga > (run_key(key) ? kBigRun : kBigGroup);
-  };
-  uint32_t* C = reinterpret_cast<uint32_t*>(scratchAll + S.elemOff);  // candidates: bin << 17 | rel
-  uint32_t* T = C + E;                                                 // targets: bin << 17 | rel
+  uint32_t* C = reinterpret_cast<uint32_t*>(scratchAll + S.elemOff);  // candidates: cls << 17 | rel
+  uint32_t* T = C + E;                                                 // targets: rel
+  uint32_t* BK = runBkt + (S.s0 - matchBase);                          // run table: runs by next byte
   __syncthreads();
 
   for (uint32_t gi = 0; gi < ng; gi++) {
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
+    const uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
+    const bool lpfG = lpf_group(compact, small, ga, S.w0, predLo, src);
+    if (tid == 0) s_mixed = 0;
+    __syncthreads();
+    if (run_key(gKey)) {
+      for (uint32_t s = ga + tid; s < gb; s += kFindThreads)
+        if (src.ld4(S.w0 + slot_pos(compact, small, s)) != gKey) s_mixed = 1;
+      __syncthreads();
+    }
+    if (run_key(gKey) && !s_mixed) {
+      // ---- a run-key group: its members are the positions with at least 4
+      // bytes of a run of v left, so its runs are the maximal stretches of consecutive member
+      // positions.  Run table (position order): C[ga + k] = start rel | next byte a << 17 (kAEnd at
+      // the block end), T[ga + k] = run length L (exact, within the block); BK: run indices by a.
+      const uint32_t v = gKey & 0xFFu;
+      // A. runs: a member whose predecessor position is not a member starts one (block-wide scan);
+      //    C[ga + k] = its start, T[ga + k] = its first slot; a target member keeps its run index in lm
+      uint32_t base = 0;
+      for (uint32_t t0 = ga; t0 < gb; t0 += kFindThreads) {
+        const uint32_t s = t0 + tid;
+        const bool inG = s < gb;
+        const uint32_t r = inG ? slot_pos(compact, small, s) : 0u;
+        const bool first = inG && (s == ga || slot_pos(compact, small, s - 1) + 1u != r);
+        uint32_t tot = 0;
+        const uint32_t k = base + block_excl_scan(first ? 1u : 0u, s_wsum, &tot);
+        if (first) {
+          C[ga + k] = r;
+          T[ga + k] = s;
+        }
+        if (inG && is_target(s, ga, S.w0 + r, gKey, lpfG)) lm[S.w0 + r - matchBase] = first ? k : k - 1u;
+        base += tot;
+      }
+      if (tid == 0) s_nRuns = base;
+      for (uint32_t k = tid; k <= kAEnd; k += kFindThreads) s_cur[0][k] = 0;
+      __threadfence_block();
+      __syncthreads();
+      const uint32_t nRuns = s_nRuns;
+      //    then each run's end (its members are consecutive positions: the run ends 4 bytes after its
+      //    last member, unless that is the window's last position and the run goes on) and next byte:
+      //    C[ga + k] = start | a << 17 (kAEnd at the block end), T[ga + k] = length
+      for (uint32_t k0 = 0; k0 < nRuns; k0 += kFindThreads) {
+        const uint32_t k = k0 + tid;
+        uint32_t r = 0, sFirst = 0, sNext = 0;
+        if (k < nRuns) {
+          r = C[ga + k];
+          sFirst = T[ga + k];
+          sNext = k + 1 < nRuns ? T[ga + k + 1] : gb;
+        }
+        __syncthreads();
+        if (k < nRuns) {
+          const uint32_t lastRel = r + (sNext - 1u - sFirst);
+          uint64_t e = S.w0 + lastRel + 4;
+          if (S.w0 + lastRel + 1 == S.s1) {
+            while (e + 4 <= B.end) {
+              const uint32_t d = src.ld4(e) ^ gKey;
+              if (d) {
+                e += (uint32_t)__builtin_ctz(d) >> 3;
+                break;
+              }
+              e += 4;
+            }
+            while (e < B.end && (src.ld4(e) & 0xFFu) == v) e++;
+          }
+          if (e > B.end) e = B.end;
+          const uint32_t a = e < B.end ? (src.ld4(e) & 0xFFu) : kAEnd;
+          C[ga + k] = r | (a << 17);
+          T[ga + k] = (uint32_t)(e - (S.w0 + r));
+        }
+        __syncthreads();
+      }
+      __threadfence_block();
+      __syncthreads();
+      if (nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
+      // B. buckets by next byte
+      for (uint32_t k = tid; k < nRuns; k += kFindThreads) atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u);
+      __syncthreads();
+      {
+        const uint32_t c0 = tid <= kAEnd ? s_cur[0][tid] : 0u;
+        const uint32_t o0 = block_excl_scan(c0, s_wsum, nullptr);
+        if (tid <= kAEnd) {
+          s_cls[tid] = o0;
+          s_cur[0][tid] = o0;
+        }
+        if (tid == 0) {
+          s_cls[kAEnd + 1] = nRuns;
+          s_next = 0;
+        }
+      }
+      __syncthreads();
+      for (uint32_t k = tid; k < nRuns; k += kFindThreads) BK[atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u)] = k;
+      __threadfence_block();
+      __syncthreads();
+      // C. every target member, 64 slots per step
+      const uint32_t nChunks = (gb - ga + 63) / 64;
+      while (true) {
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(&s_next, 1u);
+        item = rdlane(item, 0);
+        if (item >= nChunks) break;
+        const uint32_t s = ga + item * 64 + lane;
+        const uint32_t pRel = s < gb ? slot_pos(compact, small, s) : 0u;
+        const uint64_t p = S.w0 + pRel;
+        const bool act = s < gb && is_target(s, ga, p, gKey, lpfG);
+        const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its run
+        const uint32_t ci = act ? C[ga + lo] : 0u, si = ci & 0x1FFFFu, ai = ci >> 17, Li = act ? T[ga + lo] : 0u;
+        const uint64_t ei = S.w0 + si + Li;  // p's run ends here
+        const uint32_t R = (uint32_t)(ei - p);
+        const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
+        const uint32_t limit = room < kLongCap9 ? room : kLongCap9;
+        const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
+        uint32_t bl = 0, bc = 0;  // best length, its candidate (rel)
+        auto offer = [&](uint32_t l, uint32_t c) {
+          if (l > bl || (l == bl && c > bc)) {
+            bl = l;
+            bc = c;
+          }
+        };
+        const uint32_t need = Li < limit ? Li : limit;
+        int32_t wj = -1;       // a run start's walk: next run to look at when still open
+        bool open = false;
+        if (act && pRel > si) {
+          // interior: p-1 gives R bytes at distance 1; only a run of length exactly R followed by
+          // the same byte can do better (R + its common prefix after the two runs)
+          offer(R < limit ? R : limit, pRel - 1u);
+          if (R < limit && ai != kAEnd) {
+            for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
+              const uint32_t j = BK[b];
+              const uint32_t sj = C[ga + j] & 0x1FFFFu, Lj = T[ga + j];
+              if (Lj != R || sj >= pRel || sj < lbRel) continue;
+              offer(R + ext_len(S.w0 + sj + Lj, ei, limit - R), sj);
+            }
+          }
+        } else if (act) {
+          // run start: every earlier run of length >= need offers its position with need bytes
+          // left (more when the two runs are followed by the same bytes); the nearest such run,
+          // or failing any, the longest stretch the window holds
+          if (Li < limit && ai != kAEnd) {
+            for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
+              const uint32_t j = BK[b];
+              const uint32_t sj = C[ga + j] & 0x1FFFFu, Lj = T[ga + j];
+              if (j >= lo || Lj < Li) continue;
+              const uint32_t c = sj + Lj - Li;
+              if (c < lbRel) continue;
+              offer(Li + ext_len(S.w0 + sj + Lj, ei, limit - Li), c);
+            }
+          }
+          // the walk, nearest run first: a few steps per lane ...
+          wj = (int32_t)lo - 1;
+          open = true;
+          for (int it = 0; it < 16 && open; it++) {
+            if (wj < 0) {
+              open = false;
+              break;
+            }
+            const uint32_t sj = C[ga + wj] & 0x1FFFFu, ej = sj + T[ga + wj];
+            if (ej < lbRel + 4u) {  // no member of this run (or an earlier one) in the window
+              open = false;
+              break;
+            }
+            const uint32_t rHi = ej - (sj > lbRel ? sj : lbRel);
+            if (rHi >= need) {
+              offer(need, ej - need);
+              open = false;
+              break;
+            }
+            offer(rHi, ej - rHi);
+            wj--;
+          }
+        }
+        // ... and the rare long walks by the whole wavefront, 64 runs per step
+        uint64_t pend = __ballot(open);
+        while (pend) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(pend);
+          pend &= pend - 1;
+          int32_t jj = (int32_t)rdlane((uint32_t)wj, t);
+          const uint32_t nd = rdlane(need, t), lb = rdlane(lbRel, t);
+          uint32_t best = 0;  // len << 17 | candidate
+          while (jj >= 0) {
+            const int32_t k = jj - (int32_t)lane;
+            const bool ok = k >= 0;
+            const uint32_t sj = ok ? C[ga + k] & 0x1FFFFu : 0u;
+            const uint32_t ej = ok ? sj + T[ga + k] : 0u;
+            const bool inW = ok && ej >= lb + 4u;
+            const uint32_t rHi = inW ? ej - (sj > lb ? sj : lb) : 0u;
+            const uint64_t hit = __ballot(inW && rHi >= nd);
+            const uint64_t stop = hit | __ballot(!inW);
+            const uint32_t f = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // nearest stop
+            uint32_t key = 0;
+            if (inW && lane < f) key = (rHi << 17) | (ej - rHi);
+            if (inW && lane == f && rHi >= nd) key = (nd << 17) | (ej - nd);
+            key = 0xFFFFFFFFu - wave_min_u32(0xFFFFFFFFu - key);
+            best = key > best ? key : best;
+            if (stop) break;
+            jj -= 64;
+          }
+          if (lane == t) offer(best >> 17, best & 0x1FFFFu);
+        }
+        if (act) lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (pRel - bc) : 0u;
+      }
+      __syncthreads();
+      continue;
+      }
+    }
+
+    // ---- any other group: regrouped by class
     for (uint32_t k = tid; k < 2 * kBins; k += kFindThreads) (&s_cur[0][0])[k] = 0;
     __syncthreads();
-    // counts per bin (candidates: the whole group; targets: pass 1's big ones)
+    // counts per class (candidates: the whole group; targets: pass 1's big ones)
     for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
       const uint32_t r = slot_pos(compact, small, s);
       const uint64_t q = S.w0 + r;
-      const uint32_t key = src.ld4(q);
-      const uint32_t b = bin_of(q, key);
-      atomicAdd(&s_cur[0][b], 1u);
-      if (is_target(s, ga, q, key)) atomicAdd(&s_cur[1][b], 1u);
+      const uint32_t c = cls_of(q);
+      atomicAdd(&s_cur[0][c], 1u);
+      if (is_target(s, ga, q, gKey, lpfG)) atomicAdd(&s_cur[1][c], 1u);
     }
     __syncthreads();
     {
@@ -2308,24 +2552,17 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     for (uint32_t s = ga + tid; s < gb; s += kFindThreads) {
       const uint32_t r = slot_pos(compact, small, s);
       const uint64_t q = S.w0 + r;
-      const uint32_t key = src.ld4(q);
-      const uint32_t b = bin_of(q, key);
-      C[ga + atomicAdd(&s_cur[0][b], 1u)] = (b << 17) | r;
-      if (is_target(s, ga, q, key)) T[ga + atomicAdd(&s_cur[1][b], 1u)] = (b << 17) | r;
+      const uint32_t c = cls_of(q);
+      C[ga + atomicAdd(&s_cur[0][c], 1u)] = (c << 17) | r;
+      if (is_target(s, ga, q, gKey, lpfG)) T[ga + atomicAdd(&s_cur[1][c], 1u)] = r;
     }
     __threadfence_block();
     __syncthreads();
 
-    // 2. LM of every big target, chunks of 64 targets in bin order.  A lane scans a range of C:
-    //    non-run key: every non-run bin but its own class (p's predecessor is a target of this block:
-    //      those candidates carry from p-1);
-    //    run interior (p-1 in the run): p-1 gives R(p) at distance 1, so only the run STARTS of its R
-    //      bin can do better (R bytes + the next ones); with R(p) >= limit nothing can;
-    //    run start: its R bin (one member per earlier run at least R long, the nearest position of
-    //      that run with R in common); when none is usable, every run member (fallback).
+    // 2. LM of every big target: chunks of up to 64 targets, taken class by class; a class's last,
+    //    partial chunk is filled up with the next classes' first targets (mixed: scan all, filter)
     const uint32_t nT = s_tcls[kBins];
     const uint32_t nChunks = (nT + 63) / 64;
-    const uint32_t runLo = s_cls[kBinRun0], runHi = s_cls[kBins];
     while (true) {
       uint32_t item = 0;
       if (lane == 0) item = atomicAdd(&s_next, 1u);
@@ -2333,92 +2570,64 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       if (item >= nChunks) break;
       const uint32_t t = item * 64 + lane;
       const bool act = t < nT;
-      const uint32_t te = act ? T[ga + t] : 0u;
-      const uint32_t pRel = te & 0x1FFFFu, myBin = act ? te >> 17 : kNoBin;
+      const uint32_t pRel = act ? T[ga + t] : 0u;
       const uint64_t p = S.w0 + pRel;
+      const uint32_t myCls = act ? cls_of(p) : kClsNone + 1;
+      // p's own class is excluded only when p-1 is a target of this block (its result carries to p)
+      const uint32_t exCls = act && p > B.start && myCls < kClsNone ? myCls : kClsNone + 1;
       const uint32_t me0 = act ? src.ld4(p) : 0u, me1 = act ? src.ld4(p + 4) : 0u, me2 = act ? src.ld4(p + 8) : 0u;
       const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
       const uint32_t limit = room < kLongCap9 ? room : kLongCap9;
       const uint32_t cap12 = limit < 12u ? limit : 12u;
       const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
-      const bool isRun = act && myBin >= kBinRun0;
-      const uint32_t rb = isRun ? (myBin - kBinRun0) >> 1 : 0u;
-      const bool runStart = isRun && ((myBin - kBinRun0) & 1u);
-      const uint32_t R = isRun ? rb + 4u : 0u;
-      uint32_t bestKey = 0, lo = 0, hi = 0, exBin = kNoBin;
-      if (act && !isRun) {
-        lo = 0;
-        hi = runLo;
-        // p's own class is excluded only when p-1 is a target of this block (its result carries to p)
-        if (p > B.start && myBin < kClsNone) exBin = myBin;
-      } else if (isRun && !runStart) {
-        bestKey = ((R < limit ? R : limit) << 17) | (pRel - 1u);
-        if (R < limit) {
-          lo = s_cls[myBin + 1];
-          hi = s_cls[myBin + 2];
-        }
-      } else if (runStart) {
-        lo = s_cls[myBin - 1];
-        hi = s_cls[myBin + 1];
+      // candidate ranges of C: one class for the whole wavefront -> skip it; else scan everything
+      const uint32_t e0 = rdlane(exCls, 0);
+      const bool one = __ballot(act && exCls != e0) == 0 && e0 < kClsNone;
+      uint32_t r0a = ga, r0b = gb, r1a = gb, r1b = gb;
+      if (one) {
+        r0b = ga + s_cls[e0];
+        r1a = ga + s_cls[e0 + 1];
       }
-      // one candidate for the lanes whose range holds C index ci: entry ej, first 12 bytes k0..k2
-      auto take = [&](uint32_t ci, uint32_t clo, uint32_t chi, uint32_t ej, uint32_t k0, uint32_t k1, uint32_t k2) {
-        const uint32_t c = ej & 0x1FFFFu, cb = ej >> 17;
-        const bool ok = ci >= clo && ci < chi && cb != exBin && c < pRel && c >= lbRel && k0 == me0;
-        const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
-        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
-        const uint32_t z = min(z1, 32u + min(z2, 32u));
-        uint32_t lcp = min(4u + (z >> 3), cap12);
-        if (ok && lcp == 12u && limit > 12u) {
-          // both share 12 bytes (a member of p's own R bin shares R): the exact prefix, unless the 4
-          // bytes ending at the current best length already differ (then it cannot win)
-          const uint64_t cc = S.w0 + c;
-          const uint32_t bl = bestKey >> 17;
-          if (isRun && cb >= kBinRun0 && ((cb - kBinRun0) >> 1) == rb) lcp = max(12u, min(R, limit));
-          bool open = !(bl > lcp && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
-          while (open && lcp < limit) {
-            const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
-            if (x) {
-              lcp += (uint32_t)__builtin_ctz(x) >> 3;
-              open = false;
-            } else {
-              lcp += 4;
+      uint32_t bestKey = 0;
+      for (int part = 0; part < 2; part++) {
+        const uint32_t lo = part == 0 ? r0a : r1a, hi = part == 0 ? r0b : r1b;
+        for (uint32_t base = lo; base < hi; base += 64) {
+          const uint32_t ci = base + lane;
+          const uint32_t ce = ci < hi ? C[ci] : 0xFFFFFFFFu;
+          const uint32_t cr = ce & 0x1FFFFu;
+          const uint64_t cp = S.w0 + (ci < hi ? cr : 0u);
+          const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
+          const uint32_t n = hi - base < 64u ? hi - base : 64u;
+          for (uint32_t j = 0; j < n; j++) {
+            const uint32_t ej = rdlane(ce, j), k0 = rdlane(f0, j), k1 = rdlane(f1, j), k2 = rdlane(f2, j);
+            const uint32_t c = ej & 0x1FFFFu;
+            const bool ok = act && c < pRel && c >= lbRel && (ej >> 17) != exCls && k0 == me0;
+            const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
+            const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+            const uint32_t z = min(z1, 32u + min(z2, 32u));
+            uint32_t lcp = min(4u + (z >> 3), cap12);
+            if (ok && lcp == 12u && limit > 12u) {
+              // both share 12 bytes: the exact prefix, unless the 4 bytes ending at the current best
+              // length already differ (then it stays below the best and cannot win)
+              const uint64_t cc = S.w0 + c;
+              const uint32_t bl = bestKey >> 17;
+              bool open = !(bl > 12u && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
+              while (open && lcp < limit) {
+                const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
+                if (x) {
+                  lcp += (uint32_t)__builtin_ctz(x) >> 3;
+                  open = false;
+                } else {
+                  lcp += 4;
+                }
+              }
+              if (lcp > limit) lcp = limit;
             }
-          }
-          if (lcp > limit) lcp = limit;
-        }
-        const uint32_t key = ok ? (lcp << 17) | c : 0u;
-        bestKey = key > bestKey ? key : bestKey;
-      };
-      // the wave scans the union of its lanes' ranges; a wave of one class skips that class's bin
-      auto scan = [&](uint32_t clo, uint32_t chi) {
-        const uint32_t wlo = wave_min_u32(clo < chi ? clo : 0xFFFFFFFFu);
-        const uint32_t whi = 0xFFFFFFFFu - wave_min_u32(clo < chi ? 0xFFFFFFFFu - chi : 0xFFFFFFFFu);
-        if (wlo >= whi) return;
-        const uint32_t e0 = rdlane(exBin, (uint32_t)__builtin_ctzll(__ballot(act) | (1ull << 63)));
-        const bool one = e0 != kNoBin && __ballot(act && exBin != e0) == 0;
-        uint32_t r0a = wlo, r0b = whi, r1a = whi, r1b = whi;
-        if (one) {
-          r0b = min(whi, s_cls[e0]);
-          r1a = max(wlo, s_cls[e0 + 1]);
-        }
-        for (int part = 0; part < 2; part++) {
-          const uint32_t a = part == 0 ? r0a : r1a, b = part == 0 ? r0b : r1b;
-          for (uint32_t base = a; base < b; base += 64) {
-            const uint32_t ci = base + lane;
-            const uint32_t ce = ci < b ? C[ga + ci] : 0xFFFFFFFFu;
-            const uint64_t cp = S.w0 + (ci < b ? ce & 0x1FFFFu : 0u);
-            const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
-            const uint32_t n = b - base < 64u ? b - base : 64u;
-            for (uint32_t j = 0; j < n; j++)
-              take(base + j, clo, chi, rdlane(ce, j), rdlane(f0, j), rdlane(f1, j), rdlane(f2, j));
+            const uint32_t key = ok ? (lcp << 17) | c : 0u;
+            bestKey = key > bestKey ? key : bestKey;
           }
         }
-      };
-      scan(lo, hi);
-      // run starts with no usable member of their R bin: every run member
-      const bool fb = runStart && bestKey == 0u;
-      if (__ballot(fb)) scan(fb ? runLo : 0u, fb ? runHi : 0u);
+      }
       if (act) {
         const uint32_t bl = bestKey >> 17;
         lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (uint32_t)(pRel - (bestKey & 0x1FFFFu)) : 0u;
@@ -4740,7 +4949,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, resolve);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
@@ -4761,7 +4970,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, resolve);
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, resolve);
       hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,

@@ -88,9 +88,19 @@ def test_bench_gpus2_dry_run_starts_two_ranks():
 
 def test_range_generators_are_slices_of_one_input():
     from smallz4_amd import synth
-    a = synth.zeros_urandom_range(0, 1 << 20)
+    import numpy as np
+    a = synth.zeros_urandom_range(0, 40 << 20)
     assert synth.zeros_urandom_range(123457, 777777) == a[123457:777777]
-    assert a[:131072] == bytes(131072) and a[131072:262144] != bytes(131072)
+    cell = synth.ZU_CELL
+    assert synth.zeros_urandom_range(cell - 5000, cell + 5000) == a[cell - 5000:cell + 5000]
+    # configs[4]'s layout: half the bytes zero, zero runs starting at every phase of the 256 KiB grid
+    x = np.frombuffer(a, dtype=np.uint8)
+    assert 0.45 < (x == 0).mean() < 0.56
+    z = np.zeros(len(x) // 4096, dtype=bool)
+    z[:] = (x[:len(z) * 4096].reshape(-1, 4096) == 0).all(axis=1)  # 4 KiB pages of zeros
+    starts = np.flatnonzero(z[1:] & ~z[:-1]) + 1
+    phases = set(((starts * 4096) % 262144) // 32768)
+    assert len(starts) > 50 and phases == set(range(8))
     seg = synth.ENWIK9_SEGMENT
     x = synth.enwik9_like_range(seg - 1000, seg + 1000)
     assert x == synth.enwik9_like_range(seg - 1000, seg) + synth.enwik9_like_range(seg, seg + 1000)

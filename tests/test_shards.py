@@ -61,6 +61,7 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
         data = synth.zeros_urandom_range(lo, hi, seed=10)
     before = compressor.device_bytes()
     part = compressor.compress_blocks(data, bs, 65535, header="none")
+    footprint = compressor.device_bytes()  # before the decoder's own scratch joins it
     spans = _spans(part)
     assert len(spans) == (len(data) + bs - 1) // bs
     assert _device_roundtrip(compressor, part, data)
@@ -75,10 +76,66 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
         o, n = spans[i]
         assert part[o:o + n] == w, i
     # HBM footprint of the context for this slice (grow-only scratch)
-    footprint = compressor.device_bytes()
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
-    assert footprint < 120 * len(data) + (1 << 30)
+    # bounded: sz4_compress_blocks_device runs 128 MiB pieces (~60-75 B of scratch per piece byte)
+    assert footprint < 16 << 30
+
+
+def test_batch_4gib_one_call_bounded_memory(compressor):
+    """4 GiB of configs[4]'s shape (zeros/urandom runs, 256 KiB blocks) in ONE sz4_compress_blocks_device
+    call: the context's scratch stays under 16 GiB (the call runs 128 MiB pieces), the frame decodes
+    back on the device, every size word walks, and sampled blocks equal the oracle's."""
+    import torch
+    bs = 262144
+    lo = 3 << 30
+    data = synth.zeros_urandom_range(lo, lo + (4 << 30), seed=10)
+    t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    cap = compressor._lib.sz4_bound(len(data), bs)
+    out = torch.empty(cap, dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    size = compressor.compress_blocks_device(t.data_ptr(), len(data), out.data_ptr(), cap, bs, 65535, "none", stream)
+    footprint = compressor.device_bytes()
+    print(f"4 GiB in one call: context holds {footprint / 2**30:.2f} GiB")
+    assert footprint < 16 << 30
+    # round trip on the device
+    fr = torch.empty(size + 11, dtype=torch.uint8, device="cuda")
+    fr[:7] = torch.tensor(list(shard.HEADER), dtype=torch.uint8)
+    fr[7:7 + size] = out[:size]
+    fr[7 + size:] = 0
+    del out
+    dec = torch.empty(len(data), dtype=torch.uint8, device="cuda")
+    n = compressor.unlz4_device(fr.data_ptr(), fr.numel(), dec.data_ptr(), len(data), stream=stream)
+    torch.cuda.synchronize()
+    assert n == len(data) and bool(torch.equal(dec, t))
+    part = fr[7:7 + size].cpu().numpy().tobytes()
+    del fr, dec, t
+    spans = _spans(part)
+    assert len(spans) == len(data) // bs
+    sizes = compressor.last_block_sizes(len(spans))
+    assert sizes == [n for _, n in spans]
+    from concurrent.futures import ThreadPoolExecutor
+    idx = [1, len(spans) // 2 + 3, len(spans) - 1]
+    with ThreadPoolExecutor(max_workers=3) as ex:
+        want = list(ex.map(lambda i: pyoracle.oz_block(data[i * bs:(i + 1) * bs], 65535), idx))
+    for i, w in zip(idx, want):
+        o, n = spans[i]
+        assert part[o:o + n] == w, i
+
+
+def test_batch_pieces_equal_one_run(compressor):
+    """The internal pieces are invisible: a call forced into 1 MiB pieces writes the same frame (and
+    block sizes) as one run over the whole input."""
+    data = synth.enwik8_like(5 << 20, seed=91) + bytes(300000) + synth.zeros_urandom_range(0, 3 << 20)
+    whole = compressor.compress_blocks(data, 65536, 65535)
+    compressor.set_batch_chunk(1 << 20)
+    try:
+        pieces = compressor.compress_blocks(data, 65536, 65535)
+        sizes = compressor.last_block_sizes(200)
+    finally:
+        compressor.set_batch_chunk(0)
+    assert pieces == whole
+    assert sum(sizes) == len(whole) - 11 and len(sizes) == (len(data) + 65535) // 65536
 
 
 @pytest.mark.parametrize("workload,mb,sample", [("enwik9", 8, 16), ("zeros_urandom", 4, 2)])
@@ -95,9 +152,13 @@ def test_bench_two_ranks_shard_one_input(workload, mb, sample):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, SZ4_BENCH_SHARE_DEVICE="1")
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", workload,
-                        "--mb", str(mb), "--steps", "2", "--warmup", "1", "--verify-blocks", str(sample),
-                        "--no-stream"], capture_output=True, text=True, timeout=400, cwd=root, env=env)
+                        "--mb", str(mb), "--steps", "2", "--warmup", "1", "--verify-seconds", "15",
+                        "--cpu-seconds", "1", "--no-stream"], capture_output=True, text=True, timeout=400, cwd=root,
+                       env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert rec["n_gpus"] == 2 and rec["config"]["input_bytes"] == 2 * mb * 1_000_000, rec
-    assert rec["byte_diff"] == 0 and rec["blocks_verified"] >= 2 * sample and rec["roundtrip_ok"], rec
+    assert rec["byte_diff"] == 0 and rec["blocks_verified"] >= sample and rec["roundtrip_ok"], rec
+    # the N>1 line carries the CPU baseline (rank 0) and its per-GPU rate, like the N=1 line
+    assert rec["cpu_baseline"]["value"] > 0 and rec["value_per_gpu"] * 2 == pytest.approx(rec["value"], rel=1e-3)
+    assert rec["verify"]["verify_budget_s"] == 15

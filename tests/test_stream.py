@@ -53,6 +53,36 @@ def test_chunk_boundaries_match_oracle(chunked, chain, case):
     assert chunked.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
 
 
+@pytest.mark.parametrize("chain", [5, 65535])
+def test_multi_block_chunks_carry_state(compressor, chain):
+    """Chunks of two and three 4 MiB blocks: the ghost slot then carries the intervals of a chunk's
+    LAST block (B.prev = nb) across the boundary; a zero run crosses the first chunk boundary and
+    another lies inside a chunk.  The whole frame against the oracle."""
+    data = (synth.enwik8_like(2 * M - 50000, seed=92) + bytes(120000) + synth.enwik8_like(M, seed=93) +
+            bytes(90000) + synth.enwik8_like(2 * M + 12345, seed=94))
+    for chunk in (2 * M, 3 * M):
+        compressor.set_stream_chunk(chunk)
+        try:
+            assert compressor.lz4(data, chain) == pyoracle.oz_lz4(data, chain), chunk
+        finally:
+            compressor.set_stream_chunk(0)
+
+
+def test_stream_rejects_oversized_reads(compressor):
+    """A read callback that returns more bytes than it was asked for is an error, not an overrun."""
+    data = synth.enwik8_like(300000, seed=95)
+    with pytest.raises(ValueError):
+        compressor.lz4_stream(lambda n: data, lambda b: None, 65535)
+
+
+def test_decoder_stream_rejects_huge_block_word(compressor):
+    """A size word larger than any LZ4 block is corrupt (checked before anything is reserved)."""
+    from smallz4_amd._native import NativeError
+    frame = bytes([0x04, 0x22, 0x4D, 0x18, 0x40, 0x70, 0xDF]) + (0x7FFFFFF0).to_bytes(4, "little") + bytes(64)
+    with pytest.raises(NativeError, match="larger than any LZ4 block"):
+        _decode_stream(compressor, frame)
+
+
 @pytest.mark.parametrize("legacy", [False, True])
 @pytest.mark.parametrize("chain", [3, 6])
 def test_chunked_dictionary(chunked, chain, legacy):
