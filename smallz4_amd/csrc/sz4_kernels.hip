@@ -110,7 +110,7 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
 }
 
 // DPP row (16-lane) permutations
-#if SZ4_DIAG == 3 || SZ4_DIAG == 4
+#if SZ4_DIAG >= 3
 __device__ uint64_t sz4_diag[1 << 20];
 extern "C" int sz4_diag_read(uint64_t* out, uint64_t n)
 {
@@ -721,24 +721,20 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
   return small ? (uint32_t)reinterpret_cast<const uint16_t*>(base)[E + s] : reinterpret_cast<const uint32_t*>(base)[E + s];
 }
 
-// An LPF group (k_find_big): a key group whose first kLpfProbe members share
-// their preceding byte -- records, markup, tables: most candidates of a target then share its
-// preceding byte too and carry from p-1, so k_find_big's left-maximal search takes its targets from
-// kLpfMin candidates on.  A function of the group start and the text, so that k_find_sorted and
-// k_find_big agree on it.  predLo: positions at or below it have no known predecessor.
+// An LPF target (k_find_big): a target whose candidates mostly share its
+// preceding byte -- records, markup, tables -- so that they carry from p-1 and k_find_big's
+// left-maximal search only visits the few others.  Decided on kLpfProbe candidates spread over the
+// group below the target: at least kLpfProbe - 2 of them share its preceding byte `cls`.
 template <class Src>
-__device__ __forceinline__ bool lpf_group(const void* compact, bool small, uint32_t gs, uint64_t w0, uint64_t predLo,
-                                          const Src& src)
+__device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint32_t gs, uint32_t slot, uint32_t cls,
+                                           uint64_t w0, uint64_t predLo, const Src& src)
 {
-  uint32_t c0 = 0;
+  uint32_t same = 0;
   for (uint32_t k = 0; k < kLpfProbe; k++) {
-    const uint64_t q = w0 + slot_pos(compact, small, gs + k);
-    if (q <= predLo) return false;
-    const uint32_t c = src.ld4(q - 1) & 0xFFu;
-    if (k == 0) c0 = c;
-    else if (c != c0) return false;
+    const uint64_t q = w0 + slot_pos(compact, small, gs + (uint32_t)((uint64_t)(slot - gs) * k / kLpfProbe));
+    same += q > predLo && (src.ld4(q - 1) & 0xFFu) == cls ? 1u : 0u;
   }
-  return true;
+  return same + 2u >= kLpfProbe;
 }
 
 template <bool kLds>
@@ -867,12 +863,14 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     // which walks in text order and prunes with the previous target's result
     // (k_find_big takes blocks without a lookback cut or shortcut intervals; there run keys go from kBigRun on)
     const bool lpfOk = B.cut == kNone && ivCount[S.block] == 0u && (B.prev == kNoBlock || ivCount[B.prev] == 0u);
-    // (a run group: its first member's key is a run key -- the group start decides, as in k_find_big)
+    // (k_find_big takes exactly the targets marked here: marked, distance 0)
+    const uint64_t predLoF = S.w0 > B.low ? S.w0 : B.low;
     const bool big = unlimited && cut == kNone && active &&
                      (slot - gs > kBigGroup ||
                       (lpfOk && slot - gs > kLpfMin &&
-                       ((slot - gs > kBigRun && run_key(src.ld4(S.w0 + slot_pos(compact, small, gs)))) ||
-                        lpf_group(compact, small, gs, S.w0, S.w0 > B.low ? S.w0 : B.low, src))));
+                       ((slot - gs > kBigRun && run_key(me0)) ||
+                        (p > predLoF &&
+                         lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, src)))));
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
@@ -1876,6 +1874,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
 
   // best match of target p (wave-uniform): carry (cLen, cDist), exact = the carry is p-1's maximum
   auto best_of = [&](uint64_t p, uint32_t cLen, uint32_t cDist, bool exact, uint32_t& bLen, uint32_t& bDist) {
+#if SZ4_DIAG == 5
+    if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[0], 1ull);
+#endif
     const uint32_t key = src.ld4(p);
     const uint32_t room = (uint32_t)(stopAbs - p);
     uint64_t lb = p > kWindow ? p - kWindow : 0;
@@ -1920,6 +1921,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       }
     }
     while (s >= gs) {
+#if SZ4_DIAG == 5
+      if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[1], 1ull);
+#endif
       const int32_t sl = s - (int32_t)lane;
       const bool inG = sl >= gs;
       const uint64_t c = inG ? S.w0 + slot_pos(compact, small, (uint32_t)sl) : 0u;
@@ -1964,6 +1968,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
   // one target per lane (a speculative batch): the same result as best_of under the same carry,
   // each lane walking its own candidates (class runs jumped with skip pointers)
   auto best_lane = [&](uint64_t p, uint32_t cLen, uint32_t cDist, uint32_t& bLen, uint32_t& bDist) {
+#if SZ4_DIAG == 5
+    atomicAdd((unsigned long long*)&sz4_diag[2], 1ull);
+#endif
     const uint32_t key = src.ld4(p);
     const uint32_t room = (uint32_t)(stopAbs - p);
     const uint64_t lb = p > kWindow ? p - kWindow : 0;  // no lookback cut on this path
@@ -1984,6 +1991,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       const int32_t gs = (int32_t)slot_gs(compact, small, E, slot);
       int32_t sl = (int32_t)slot - 1;
       while (sl >= gs) {
+#if SZ4_DIAG == 5
+        atomicAdd((unsigned long long*)&sz4_diag[3], 1ull);
+#endif
         const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)sl);
         if (c < lb) break;  // positions descend: everything farther is out of the window
         if (prune && pred_class(c) == pc) {
@@ -2075,6 +2085,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       const uint32_t aLen = mlen[q0 - 1 - matchBase], aDist = mdist[q0 - 1 - matchBase];
       if (aLen == specLen[q0 - matchBase] && aDist == sd) continue;
       walk_stretch(q0, aLen, aDist, true);
+#if SZ4_DIAG == 5
+      if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[4], 1ull);
+#endif
     }
     return;
   }
@@ -2187,6 +2200,7 @@ constexpr uint32_t kMaxBigGroups = 256;  // big, run-key and LPF groups of one s
 constexpr uint32_t kClsNone = 256;      // preceding byte class of a position without a chain predecessor
 constexpr uint32_t kBins = kClsNone + 1;
 constexpr uint32_t kAEnd = 256;         // run table: a run that reaches the block end has no next byte
+constexpr uint32_t kMaxSlotWords = (65536 + 65535 + 31) / 32;  // a window's slots as bits
 
 // exclusive prefix sums of v over the workgroup's threads (thread i: bin i); total in *tot
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* tot)
@@ -2214,7 +2228,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
                                                            uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
                                                            uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                            uint64_t matchBase, uint32_t* __restrict__ lm, uint64_t* __restrict__ segTail,
-                                                           uint32_t* __restrict__ runBkt, uint32_t resolveOnly)
+                                                           uint32_t* __restrict__ runBkt, const uint32_t* __restrict__ rankAll,
+                                                           uint32_t resolveOnly)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_groups[2 * kMaxBigGroups];
@@ -2250,26 +2265,58 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   const uint32_t E = (uint32_t)(S.s1 - S.w0);  // no intervals: every window position is a slot
   const bool small = compact_small(S);
 
-  // 1. big groups: the last slot s of a group holding a target that pass 1 handed on (more than
-  //    kBigGroup candidates, or kBigRun for a run key: the same predicate as k_find_sorted's)
-  if (tid == 0) s_ng = 0;
+  // 1. big groups: the groups of the targets pass 1 handed on (marked, distance 0), found through their
+  //    slots (rank): their starts as a bitmap over the window's slots, collected in slot order, each
+  //    group's end by a binary search over the group starts
+  const uint32_t nTg = (uint32_t)(S.s1 - S.s0);
+  const uint32_t* rank = rankAll + S.rankOff;
+  auto handed = [&](uint64_t q) -> bool {  // q: a target of this segment
+    const uint64_t idx = q - matchBase;
+    return ((longBits[idx >> 5] >> (idx & 31)) & 1u) && mlen[idx] == kLongMatch && mdist[idx] == 0u;
+  };
+  const uint32_t gWords = (E + 31) / 32;
+  uint32_t* s_gmap = win;  // (the window is loaded only after this: its buffer holds E bits many times over)
+  for (uint32_t w = tid; w < gWords; w += kFindThreads) s_gmap[w] = 0;
   __syncthreads();
-  const uint64_t predLo0 = S.w0 > B.low ? S.w0 : B.low;
-  const Bytes<false> gsrc{in};
-  for (uint32_t s = tid; s < E; s += kFindThreads) {
-    const uint32_t g = slot_gs(compact, small, E, s);
-    if (s - g > kLpfMin && (s + 1 == E || slot_gs(compact, small, E, s + 1) != g) &&
-        (s - g > kBigGroup || (s - g > kBigRun && run_key(gload4(in, S.w0 + slot_pos(compact, small, g)))) ||
-         lpf_group(compact, small, g, S.w0, predLo0, gsrc))) {
-      const uint32_t k = atomicAdd(&s_ng, 1u);
-      if (k < kMaxBigGroups) {
-        s_groups[2 * k] = g;
-        s_groups[2 * k + 1] = s + 1;
+  for (uint32_t i = tid; i < nTg; i += kFindThreads)
+    if (handed(S.s0 + i)) {
+      const uint32_t g = slot_gs(compact, small, E, rank[i]);
+      atomicOr(&s_gmap[g >> 5], 1u << (g & 31));
+    }
+  __syncthreads();
+  uint32_t ng = 0;
+  {
+    // words per thread: ceil(4096 / 1024) = 4
+    constexpr uint32_t kPer = (kMaxSlotWords + kFindThreads - 1) / kFindThreads;
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t w = tid * kPer + k;
+      cnt += w < gWords ? (uint32_t)__builtin_popcount(s_gmap[w]) : 0u;
+    }
+    uint32_t at = block_excl_scan(cnt, s_wsum, &ng);
+    for (uint32_t k = 0; k < kPer; k++) {
+      const uint32_t w = tid * kPer + k;
+      uint32_t bits = w < gWords ? s_gmap[w] : 0u;
+      while (bits) {
+        const uint32_t b = (uint32_t)__builtin_ctz(bits);
+        bits &= bits - 1;
+        if (at < kMaxBigGroups) s_groups[2 * at] = w * 32 + b;
+        at++;
       }
     }
+    __syncthreads();
+    if (tid < ng && tid < kMaxBigGroups) {
+      const uint32_t g = s_groups[2 * tid];
+      uint32_t lo = g, hi = E - 1;  // the group's last slot: the last s with gs(s) == g
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (slot_gs(compact, small, E, mid) == g) lo = mid;
+        else hi = mid - 1;
+      }
+      s_groups[2 * tid + 1] = lo + 1;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  const uint32_t ng = s_ng;
   if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
   const uint64_t stopAbs = B.end - kTailLiterals;
 
@@ -2291,10 +2338,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
   auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
-  // the same predicate as k_find_sorted's `big` (key: the group's first member's; lpfG: an LPF group)
-  auto is_target = [&](uint32_t s, uint32_t ga, uint64_t q, uint32_t key, bool lpfG) {
-    return q >= S.s0 && (s - ga > kBigGroup || (run_key(key) && s - ga > kBigRun) || (lpfG && s - ga > kLpfMin));
-  };
+  // a member k_find_sorted handed on
+  auto is_target = [&](uint64_t q) { return q >= S.s0 && handed(q); };
   // common prefix of the texts at x and y, at most `cap` bytes (both readable that far)
   auto ext_len = [&](uint64_t x, uint64_t y, uint32_t cap) -> uint32_t {
     uint32_t k = 0;
@@ -2316,7 +2361,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   for (uint32_t gi = 0; gi < ng; gi++) {
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
     const uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
-    const bool lpfG = lpf_group(compact, small, ga, S.w0, predLo, src);
     if (tid == 0) s_mixed = 0;
     __syncthreads();
     if (run_key(gKey)) {
@@ -2344,7 +2388,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           C[ga + k] = r;
           T[ga + k] = s;
         }
-        if (inG && is_target(s, ga, S.w0 + r, gKey, lpfG)) lm[S.w0 + r - matchBase] = first ? k : k - 1u;
+        if (inG && is_target(S.w0 + r)) lm[S.w0 + r - matchBase] = first ? k : k - 1u;
         base += tot;
       }
       if (tid == 0) s_nRuns = base;
@@ -2417,7 +2461,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t s = ga + item * 64 + lane;
         const uint32_t pRel = s < gb ? slot_pos(compact, small, s) : 0u;
         const uint64_t p = S.w0 + pRel;
-        const bool act = s < gb && is_target(s, ga, p, gKey, lpfG);
+        const bool act = s < gb && is_target(p);
         const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its run
         const uint32_t ci = act ? C[ga + lo] : 0u, si = ci & 0x1FFFFu, ai = ci >> 17, Li = act ? T[ga + lo] : 0u;
         const uint64_t ei = S.w0 + si + Li;  // p's run ends here
@@ -2528,7 +2572,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       const uint64_t q = S.w0 + r;
       const uint32_t c = cls_of(q);
       atomicAdd(&s_cur[0][c], 1u);
-      if (is_target(s, ga, q, gKey, lpfG)) atomicAdd(&s_cur[1][c], 1u);
+      if (is_target(q)) atomicAdd(&s_cur[1][c], 1u);
     }
     __syncthreads();
     {
@@ -2554,7 +2598,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       const uint64_t q = S.w0 + r;
       const uint32_t c = cls_of(q);
       C[ga + atomicAdd(&s_cur[0][c], 1u)] = (c << 17) | r;
-      if (is_target(s, ga, q, gKey, lpfG)) T[ga + atomicAdd(&s_cur[1][c], 1u)] = r;
+      if (is_target(q)) T[ga + atomicAdd(&s_cur[1][c], 1u)] = r;
     }
     __threadfence_block();
     __syncthreads();
@@ -2643,7 +2687,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   //    its own key, U (unknown: a pass-1 long match, or LM at the cap) invalidates it, B (big) takes
   //    the maximum of the state and its LM.  16 wavefronts take consecutive ranges; a range's carry-in
   //    comes from the ranges before it (phase 0 summarises, phase 1 resolves).
-  const uint32_t nTg = (uint32_t)(S.s1 - S.s0);
   const uint32_t waves = kFindThreads / 64;
   const uint32_t span = ((nTg + waves - 1) / waves + 63) / 64 * 64;
   const uint32_t r0 = wave * span, r1 = r0 + span < nTg ? r0 + span : nTg;
@@ -4949,7 +4992,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, resolve);
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, resolve);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
@@ -4970,7 +5013,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, resolve);
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, resolve);
       hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
