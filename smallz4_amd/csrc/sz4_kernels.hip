@@ -697,7 +697,8 @@ constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_big / k_find_long9
 constexpr uint32_t kBigRun = 2048;    // the same for a run key (vvvv) in blocks k_find_big takes
-constexpr uint32_t kLpfMin = 256;     // ... and for any key of an LPF group (below)
+constexpr uint32_t kBigRunL = 32;     // ... in blocks above 64 KiB (k_find_big's run table is exact and cheap)
+constexpr uint32_t kLpfMin = 256;     // ... and for an LPF target (below)
 constexpr uint32_t kLpfProbe = 8;
 __device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
@@ -861,16 +862,18 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     uint32_t bestLen = 1, bestDist = 0, steps = unlimited ? 0xFFFFFFFFu : maxChain;
     // -9, a target with more than kBigGroup candidates (runs, periodic data): left to k_find_long9,
     // which walks in text order and prunes with the previous target's result
-    // (k_find_big takes blocks without a lookback cut or shortcut intervals; there run keys go from kBigRun on)
-    const bool lpfOk = B.cut == kNone && ivCount[S.block] == 0u && (B.prev == kNoBlock || ivCount[B.prev] == 0u);
-    // (k_find_big takes exactly the targets marked here: marked, distance 0)
+    // In blocks without a lookback (k_find_big takes those; shortcut intervals are fine) also run-key
+    // targets and LPF targets go there; k_find_big takes exactly the targets marked here (distance 0)
+    const bool lpfOk = B.cut == kNone && B.low == B.start;
     const uint64_t predLoF = S.w0 > B.low ? S.w0 : B.low;
+    // LPF targets in blocks above 64 KiB only: a 64 KiB block's groups are small, and text gains nothing
+    // there that would pay for k_find_big's pass over the segment
+    const bool lpfBlock = B.end - B.start > 65536u;
     const bool big = unlimited && cut == kNone && active &&
                      (slot - gs > kBigGroup ||
-                      (lpfOk && slot - gs > kLpfMin &&
-                       ((slot - gs > kBigRun && run_key(me0)) ||
-                        (p > predLoF &&
-                         lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, src)))));
+                      (lpfOk && ((run_key(me0) && slot - gs > (lpfBlock ? kBigRunL : kBigRun)) ||
+                                 (lpfBlock && slot - gs > kLpfMin && p > predLoF &&
+                                  lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, src)))));
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
@@ -2201,6 +2204,8 @@ constexpr uint32_t kClsNone = 256;      // preceding byte class of a position wi
 constexpr uint32_t kBins = kClsNone + 1;
 constexpr uint32_t kAEnd = 256;         // run table: a run that reaches the block end has no next byte
 constexpr uint32_t kMaxSlotWords = (65536 + 65535 + 31) / 32;  // a window's slots as bits
+constexpr uint32_t kNoScan = 0xFFFFFFFFu;
+constexpr uint32_t kLmUnknown = 0xFFFFu;  // LM length: at pass 1's cap (longer possible): pass 2 decides
 
 // exclusive prefix sums of v over the workgroup's threads (thread i: bin i); total in *tot
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, uint32_t* tot)
@@ -2220,20 +2225,39 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   return base + incl - v;
 }
 
+#if SZ4_DIAG == 6
+#define SZ4_D6(k)                                                                                   \
+  do {                                                                                            \
+    if (threadIdx.x == 0) {                                                                       \
+      const uint64_t now = __builtin_readcyclecounter();                                          \
+      atomicAdd((unsigned long long*)&sz4_diag[k], (unsigned long long)(now - d6t));              \
+      d6t = now;                                                                                  \
+    }                                                                                             \
+  } while (0)
+#define SZ4_D6C(k, v) atomicAdd((unsigned long long*)&sz4_diag[k], (unsigned long long)(v))
+#else
+#define SZ4_D6(k) \
+  do {            \
+  } while (0)
+#define SZ4_D6C(k, v) \
+  do {                \
+  } while (0)
+#endif
 template <bool kLds>
 __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
-                                                           const Block* __restrict__ blocks,
+                                                           const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                            const uint32_t* __restrict__ ivCount,
                                                            const uint2* __restrict__ compactAll, uint2* __restrict__ scratchAll,
                                                            uint32_t* __restrict__ longBits, const uint32_t* __restrict__ segLong,
                                                            uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                            uint64_t matchBase, uint32_t* __restrict__ lm, uint64_t* __restrict__ segTail,
                                                            uint32_t* __restrict__ runBkt, const uint32_t* __restrict__ rankAll,
-                                                           uint32_t resolveOnly)
+                                                           uint32_t* __restrict__ longFlag, uint32_t resolveOnly)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_groups[2 * kMaxBigGroups];
-  __shared__ uint32_t s_ng, s_next, s_mixed, s_nRuns;
+  __shared__ uint32_t s_ng, s_next, s_mixed, s_nRuns, s_scanRun, s_niv;
+  __shared__ uint64_t s_ivLo[kMaxIv], s_ivHi[kMaxIv], s_ivA[kMaxIv], s_ivLa[kMaxIv];  // this block's intervals
   __shared__ uint32_t s_cls[kBins + 1], s_tcls[kBins + 1];  // bin starts (candidates, targets); run buckets
   __shared__ uint32_t s_cur[2][kBins];                      // counts, then scatter cursors
   __shared__ uint32_t s_wsum[kFindThreads / 64];
@@ -2241,9 +2265,31 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   __shared__ uint64_t s_outKey[kFindThreads / 64];
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
-  if (B.cut != kNone || ivCount[S.block] != 0u || (B.prev != kNoBlock && ivCount[B.prev] != 0u))
+  if (B.cut != kNone || B.low != B.start)
     return;  // uniform over the workgroup (the resolve launch returns here for every segment of the block)
   const uint32_t tid = threadIdx.x, lane = tid & 63;
+  // the block's shortcut intervals (smallz4.h:631-643): their positions are neither inserted nor searched
+  if (tid == 0) s_niv = ivCount[S.block] < kMaxIv ? ivCount[S.block] : kMaxIv;
+  __syncthreads();
+  const uint32_t niv = s_niv;
+  for (uint32_t j = tid; j < niv; j += kFindThreads) {
+    const Interval x = ivAll[(uint64_t)S.block * kMaxIv + j];
+    s_ivLo[j] = x.lo;
+    s_ivHi[j] = x.hi;
+    s_ivA[j] = x.a;
+    s_ivLa[j] = x.La;
+  }
+  __syncthreads();
+  auto excluded = [&](uint64_t q) -> bool {
+    for (uint32_t j = 0; j < niv; j++)
+      if (q >= s_ivLo[j] && q < s_ivHi[j]) return true;
+    return false;
+  };
+  auto iv_starting_at = [&](uint64_t q) -> int32_t {
+    for (uint32_t j = 0; j < niv; j++)
+      if (s_ivLo[j] == q) return (int32_t)j;
+    return -1;
+  };
   if (!resolveOnly && tid == 0) {
     // the state after this segment's last target for the next segment's resolve launch, as it stands
     // when no target here is left to this kernel (no big group, or more than fit): the last target's
@@ -2262,9 +2308,17 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   if (!segLong[blockIdx.x]) return;  // uniform
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
   const void* compact = compactAll + S.elemOff;
-  const uint32_t E = (uint32_t)(S.s1 - S.w0);  // no intervals: every window position is a slot
+  uint32_t E = (uint32_t)(S.s1 - S.w0);  // window positions minus interval positions: the slots
+  for (uint32_t j = 0; j < niv; j++) {
+    const uint64_t lo = s_ivLo[j] > S.w0 ? s_ivLo[j] : S.w0, hi = s_ivHi[j] < S.s1 ? s_ivHi[j] : S.s1;
+    if (lo < hi) E -= (uint32_t)(hi - lo);
+  }
   const bool small = compact_small(S);
 
+#if SZ4_DIAG == 6
+  uint64_t d6t = __builtin_readcyclecounter();
+  if (tid == 0 && !resolveOnly) SZ4_D6C(15, 1);
+#endif
   // 1. big groups: the groups of the targets pass 1 handed on (marked, distance 0), found through their
   //    slots (rank): their starts as a bitmap over the window's slots, collected in slot order, each
   //    group's end by a binary search over the group starts
@@ -2320,6 +2374,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
   const uint64_t stopAbs = B.end - kTailLiterals;
 
+  if (!resolveOnly) SZ4_D6(0);
   // the second launch only resolves: a segment's first big targets need its predecessor segment's
   // last results, final after the first launch
   if (!resolveOnly) {
@@ -2336,8 +2391,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     }
   }
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
-  // class of a window position: its preceding byte, or kClsNone (then it is always left-maximal)
-  auto cls_of = [&](uint64_t q) -> uint32_t { return q <= predLo ? kClsNone : (src.ld4(q - 1) & 0xFFu); };
+  // class of a window position: its preceding byte, or kClsNone when that is not a chain position
+  // (then the position is always left-maximal)
+  auto cls_of = [&](uint64_t q) -> uint32_t {
+    return q <= predLo || excluded(q - 1) ? kClsNone : (src.ld4(q - 1) & 0xFFu);
+  };
   // a member k_find_sorted handed on
   auto is_target = [&](uint64_t q) { return q >= S.s0 && handed(q); };
   // common prefix of the texts at x and y, at most `cap` bytes (both readable that far)
@@ -2358,6 +2416,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   uint32_t* BK = runBkt + (S.s0 - matchBase);                          // run table: runs by next byte
   __syncthreads();
 
+  SZ4_D6(1);
   for (uint32_t gi = 0; gi < ng; gi++) {
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
     const uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
@@ -2369,13 +2428,20 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       __syncthreads();
     }
     if (run_key(gKey) && !s_mixed) {
-      // ---- a run-key group: its members are the positions with at least 4
-      // bytes of a run of v left, so its runs are the maximal stretches of consecutive member
-      // positions.  Run table (position order): C[ga + k] = start rel | next byte a << 17 (kAEnd at
-      // the block end), T[ga + k] = run length L (exact, within the block); BK: run indices by a.
+      // ---- a run-key group: its members are the chain positions with at
+      // least 4 bytes of a run of v left.  A "piece" is a maximal stretch of consecutive member
+      // positions: a whole run, or the part of one before / after the positions the same-letter
+      // shortcut left out (an interval), or the part inside the window.  Piece table (position
+      // order): C[ga + k] = first rel | next byte a << 17 (the byte after the RUN, kAEnd at the block
+      // end); T[ga + k] = R(first) (bytes of v from it, exact) | extra << 24 | kind << 30, kind 0: the
+      // piece ends with its run (last = end - 4), 1: an interval follows (last = first + extra),
+      // 2: the window ends inside it (last = s1 - 1).  BK: piece indices by a.  Every target's result is
+      // exact by itself (all its candidates are considered), so it is written as final.
       const uint32_t v = gKey & 0xFFu;
-      // A. runs: a member whose predecessor position is not a member starts one (block-wide scan);
-      //    C[ga + k] = its start, T[ga + k] = its first slot; a target member keeps its run index in lm
+      SZ4_D6(6);
+      if (tid == 0) SZ4_D6C(14, 1);
+      // A. pieces: a member whose predecessor position is not a member starts one (block-wide scan);
+      //    C[ga + k] = its first, T[ga + k] = its first slot; a target member keeps its piece in lm
       uint32_t base = 0;
       for (uint32_t t0 = ga; t0 < gb; t0 += kFindThreads) {
         const uint32_t s = t0 + tid;
@@ -2391,14 +2457,18 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         if (inG && is_target(S.w0 + r)) lm[S.w0 + r - matchBase] = first ? k : k - 1u;
         base += tot;
       }
-      if (tid == 0) s_nRuns = base;
+      if (tid == 0) {
+        s_nRuns = base;
+        s_scanRun = kNoScan;
+      }
       for (uint32_t k = tid; k <= kAEnd; k += kFindThreads) s_cur[0][k] = 0;
       __threadfence_block();
       __syncthreads();
       const uint32_t nRuns = s_nRuns;
-      //    then each run's end (its members are consecutive positions: the run ends 4 bytes after its
-      //    last member, unless that is the window's last position and the run goes on) and next byte:
-      //    C[ga + k] = start | a << 17 (kAEnd at the block end), T[ga + k] = length
+      //    each piece's run end e: 4 bytes after its last member, unless the run goes on past it --
+      //    into an interval (then to a + La, the interval's run end, and a few bytes more up to the
+      //    block end) or past the window's last position (then a scan, below)
+      bool bad = false;
       for (uint32_t k0 = 0; k0 < nRuns; k0 += kFindThreads) {
         const uint32_t k = k0 + tid;
         uint32_t r = 0, sFirst = 0, sNext = 0;
@@ -2411,27 +2481,67 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         if (k < nRuns) {
           const uint32_t lastRel = r + (sNext - 1u - sFirst);
           uint64_t e = S.w0 + lastRel + 4;
-          if (S.w0 + lastRel + 1 == S.s1) {
-            while (e + 4 <= B.end) {
-              const uint32_t d = src.ld4(e) ^ gKey;
-              if (d) {
-                e += (uint32_t)__builtin_ctz(d) >> 3;
-                break;
+          uint32_t kind = 0, extra = 0;
+          if ((src.ld4(e) & 0xFFu) == v) {
+            if (S.w0 + lastRel + 1 == S.s1) {
+              kind = 2;
+              s_scanRun = k;  // at most one piece holds the window's last position
+            } else {
+              kind = 1;
+              extra = lastRel - r;
+              const int32_t j = iv_starting_at(S.w0 + lastRel + 1);
+              if (j < 0 || extra > 63u) bad = true;
+              else {
+                e = s_ivA[j] + s_ivLa[j];
+                while (e < B.end && (src.ld4(e) & 0xFFu) == v) e++;
               }
-              e += 4;
             }
-            while (e < B.end && (src.ld4(e) & 0xFFu) == v) e++;
           }
           if (e > B.end) e = B.end;
-          const uint32_t a = e < B.end ? (src.ld4(e) & 0xFFu) : kAEnd;
-          C[ga + k] = r | (a << 17);
-          T[ga + k] = (uint32_t)(e - (S.w0 + r));
+          C[ga + k] = r | ((e < B.end ? (src.ld4(e) & 0xFFu) : kAEnd) << 17);
+          T[ga + k] = (uint32_t)(e - (S.w0 + r)) | (extra << 24) | (kind << 30);
         }
         __syncthreads();
       }
+      if (bad) s_mixed = 1;
       __threadfence_block();
       __syncthreads();
-      if (nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
+      //    the piece at the window's end: its run's end by wave 0, 256 bytes per step, jumping intervals
+      if (s_scanRun != kNoScan && wave == 0) {
+        const uint32_t k = s_scanRun;
+        const uint32_t r = C[ga + k] & 0x1FFFFu;
+        uint64_t e = S.s1 + 3;  // the window's last position is a member: its 4 bytes are v
+        while (e < B.end) {
+          const int32_t j = iv_starting_at(e);
+          if (j >= 0) {
+            e = s_ivA[j] + s_ivLa[j];
+            continue;
+          }
+          const uint64_t q = e + 4ull * lane;
+          const uint32_t x = q + 4 <= B.end ? src.ld4(q) ^ gKey : 0xFFFFFFFFu;
+          const uint64_t mis = __ballot(x != 0u);
+          if (mis) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(mis);
+            const uint32_t xf = rdlane(x, f);
+            const uint64_t qf = e + 4ull * f;
+            e = qf + 4 <= B.end ? qf + ((uint32_t)__builtin_ctz(xf) >> 3) : qf;
+            if (qf + 4 > B.end)
+              while (e < B.end && (src.ld4(e) & 0xFFu) == v) e++;
+            break;
+          }
+          e += 256;
+        }
+        if (e > B.end) e = B.end;
+        if (lane == 0) {
+          C[ga + k] = r | ((e < B.end ? (src.ld4(e) & 0xFFu) : kAEnd) << 17);
+          T[ga + k] = (uint32_t)(e - (S.w0 + r)) | (2u << 30);
+        }
+      }
+      __threadfence_block();
+      __syncthreads();
+      SZ4_D6(2);
+      if (tid == 0) SZ4_D6C(12, nRuns);
+      if (!s_mixed && nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
       // B. buckets by next byte
       for (uint32_t k = tid; k < nRuns; k += kFindThreads) atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u);
       __syncthreads();
@@ -2451,8 +2561,18 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       for (uint32_t k = tid; k < nRuns; k += kFindThreads) BK[atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u)] = k;
       __threadfence_block();
       __syncthreads();
+      // a piece's first, run end and last member (rel)
+      auto piece = [&](uint32_t j, uint32_t& fj, uint32_t& ej, uint32_t& lj) {
+        const uint32_t cj = C[ga + j], tj = T[ga + j];
+        fj = cj & 0x1FFFFu;
+        ej = fj + (tj & 0xFFFFFFu);
+        const uint32_t kind = tj >> 30;
+        lj = kind == 0 ? ej - 4u : kind == 1 ? fj + ((tj >> 24) & 63u) : (uint32_t)(S.s1 - 1 - S.w0);
+      };
+      SZ4_D6(3);
       // C. every target member, 64 slots per step
       const uint32_t nChunks = (gb - ga + 63) / 64;
+      bool rmq = false;
       while (true) {
         uint32_t item = 0;
         if (lane == 0) item = atomicAdd(&s_next, 1u);
@@ -2462,12 +2582,15 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t pRel = s < gb ? slot_pos(compact, small, s) : 0u;
         const uint64_t p = S.w0 + pRel;
         const bool act = s < gb && is_target(p);
-        const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its run
-        const uint32_t ci = act ? C[ga + lo] : 0u, si = ci & 0x1FFFFu, ai = ci >> 17, Li = act ? T[ga + lo] : 0u;
-        const uint64_t ei = S.w0 + si + Li;  // p's run ends here
-        const uint32_t R = (uint32_t)(ei - p);
+        const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its piece
+        if (act) SZ4_D6C(8, 1);
+        uint32_t fi = 0, eiRel = 0, li = 0;
+        if (act) piece(lo, fi, eiRel, li);
+        const uint32_t ai = act ? C[ga + lo] >> 17 : 0u;
+        const uint64_t ei = S.w0 + eiRel;  // p's run ends here
+        const uint32_t R = act ? eiRel - pRel : 0u;
         const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
-        const uint32_t limit = room < kLongCap9 ? room : kLongCap9;
+        const uint32_t limit = room;  // exact lengths (no pass-1 cap; the result goes to mlen, u32)
         const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
         uint32_t bl = 0, bc = 0;  // best length, its candidate (rel)
         auto offer = [&](uint32_t l, uint32_t c) {
@@ -2476,51 +2599,50 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             bc = c;
           }
         };
-        const uint32_t need = Li < limit ? Li : limit;
-        int32_t wj = -1;       // a run start's walk: next run to look at when still open
+        // the pieces before p's that hold a position with exactly R bytes of v left (R(c) = R(p)), and
+        // whose run is followed by the same byte: R bytes + the common prefix after the two runs
+        auto same_r = [&](uint32_t Rp) {
+          if (Rp >= limit || ai == kAEnd) return;
+          for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
+            SZ4_D6C(9, 1);
+            const uint32_t j = BK[b];
+            if (j >= lo) continue;
+            uint32_t fj, ej, lj;
+            piece(j, fj, ej, lj);
+            const uint32_t c = ej - Rp;  // its position with R(c) = Rp
+            if (c < fj || c > lj || c < lbRel) continue;
+            offer(Rp + ext_len(S.w0 + ej, ei, limit - Rp), c);
+          }
+        };
+        const uint32_t need = R < limit ? R : limit;
+        int32_t wj = -1;       // a piece start's walk: next piece to look at when still open
         bool open = false;
-        if (act && pRel > si) {
-          // interior: p-1 gives R bytes at distance 1; only a run of length exactly R followed by
-          // the same byte can do better (R + its common prefix after the two runs)
-          offer(R < limit ? R : limit, pRel - 1u);
-          if (R < limit && ai != kAEnd) {
-            for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
-              const uint32_t j = BK[b];
-              const uint32_t sj = C[ga + j] & 0x1FFFFu, Lj = T[ga + j];
-              if (Lj != R || sj >= pRel || sj < lbRel) continue;
-              offer(R + ext_len(S.w0 + sj + Lj, ei, limit - R), sj);
-            }
-          }
+        if (act && pRel > fi) {
+          // interior (p-1 is a member of its piece): p-1 gives R bytes at distance 1; a candidate with
+          // R(c) != R(p) has min(R(p), R(c)) in common, so only those with R(c) = R(p) can do better
+          offer(need, pRel - 1u);
+          same_r(R);
         } else if (act) {
-          // run start: every earlier run of length >= need offers its position with need bytes
-          // left (more when the two runs are followed by the same bytes); the nearest such run,
-          // or failing any, the longest stretch the window holds
-          if (Li < limit && ai != kAEnd) {
-            for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
-              const uint32_t j = BK[b];
-              const uint32_t sj = C[ga + j] & 0x1FFFFu, Lj = T[ga + j];
-              if (j >= lo || Lj < Li) continue;
-              const uint32_t c = sj + Lj - Li;
-              if (c < lbRel) continue;
-              offer(Li + ext_len(S.w0 + sj + Lj, ei, limit - Li), c);
-            }
-          }
-          // the walk, nearest run first: a few steps per lane ...
+          // piece start: the same, and the nearest piece holding a position with >= need bytes of v
+          // left (lcp need), or failing any, the longest stretch the window holds
+          same_r(R);
           wj = (int32_t)lo - 1;
           open = true;
           for (int it = 0; it < 16 && open; it++) {
+            SZ4_D6C(10, 1);
             if (wj < 0) {
               open = false;
               break;
             }
-            const uint32_t sj = C[ga + wj] & 0x1FFFFu, ej = sj + T[ga + wj];
-            if (ej < lbRel + 4u) {  // no member of this run (or an earlier one) in the window
+            uint32_t fj, ej, lj;
+            piece((uint32_t)wj, fj, ej, lj);
+            if (lj < lbRel) {  // no member of this piece (or an earlier one) in the window
               open = false;
               break;
             }
-            const uint32_t rHi = ej - (sj > lbRel ? sj : lbRel);
+            const uint32_t rHi = ej - (fj > lbRel ? fj : lbRel);
             if (rHi >= need) {
-              offer(need, ej - need);
+              offer(need, ej - need < lj ? ej - need : lj);
               open = false;
               break;
             }
@@ -2528,42 +2650,54 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             wj--;
           }
         }
-        // ... and the rare long walks by the whole wavefront, 64 runs per step
+        // ... and the rare long walks by the whole wavefront, 64 pieces per step
         uint64_t pend = __ballot(open);
         while (pend) {
           const uint32_t t = (uint32_t)__builtin_ctzll(pend);
           pend &= pend - 1;
           int32_t jj = (int32_t)rdlane((uint32_t)wj, t);
           const uint32_t nd = rdlane(need, t), lb = rdlane(lbRel, t);
-          uint32_t best = 0;  // len << 17 | candidate
+          uint64_t best = 0;  // len << 17 | candidate
           while (jj >= 0) {
+            if (lane == 0) SZ4_D6C(11, 1);
             const int32_t k = jj - (int32_t)lane;
             const bool ok = k >= 0;
-            const uint32_t sj = ok ? C[ga + k] & 0x1FFFFu : 0u;
-            const uint32_t ej = ok ? sj + T[ga + k] : 0u;
-            const bool inW = ok && ej >= lb + 4u;
-            const uint32_t rHi = inW ? ej - (sj > lb ? sj : lb) : 0u;
+            uint32_t fj = 0, ej = 0, lj = 0;
+            if (ok) piece((uint32_t)k, fj, ej, lj);
+            const bool inW = ok && lj >= lb;
+            const uint32_t rHi = inW ? ej - (fj > lb ? fj : lb) : 0u;
             const uint64_t hit = __ballot(inW && rHi >= nd);
             const uint64_t stop = hit | __ballot(!inW);
             const uint32_t f = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;  // nearest stop
-            uint32_t key = 0;
-            if (inW && lane < f) key = (rHi << 17) | (ej - rHi);
-            if (inW && lane == f && rHi >= nd) key = (nd << 17) | (ej - nd);
-            key = 0xFFFFFFFFu - wave_min_u32(0xFFFFFFFFu - key);
+            uint64_t key = 0;
+            if (inW && lane < f) key = ((uint64_t)rHi << 17) | (ej - rHi);
+            if (inW && lane == f && rHi >= nd) key = ((uint64_t)nd << 17) | (ej - nd < lj ? ej - nd : lj);
+            key = wave_max_u64(key);
             best = key > best ? key : best;
             if (stop) break;
             jj -= 64;
           }
-          if (lane == t) offer(best >> 17, best & 0x1FFFFu);
+          if (lane == t) offer((uint32_t)(best >> 17), (uint32_t)(best & 0x1FFFFu));
         }
-        if (act) lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (pRel - bc) : 0u;
+        if (act) {
+          // final: pass 1 and the prefix maximum below read it as an exact target
+          const uint64_t idx = p - matchBase;
+          const bool m = bl >= (uint32_t)kMinMatch;
+          mlen[idx] = m ? bl : 0u;
+          mdist[idx] = m ? (uint16_t)(pRel - bc) : (uint16_t)0;
+          atomicAnd(&longBits[idx >> 5], ~(1u << (idx & 31)));
+          rmq |= m && bl >= kRmqLen && !(pRel - bc == 1u && bl >= kSameLetter);
+        }
       }
+      if (__ballot(rmq) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
       __syncthreads();
+      SZ4_D6(5);
       continue;
       }
     }
 
     // ---- any other group: regrouped by class
+    if (tid == 0) SZ4_D6C(13, 1);
     for (uint32_t k = tid; k < 2 * kBins; k += kFindThreads) (&s_cur[0][0])[k] = 0;
     __syncthreads();
     // counts per class (candidates: the whole group; targets: pass 1's big ones)
@@ -2674,15 +2808,18 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       }
       if (act) {
         const uint32_t bl = bestKey >> 17;
-        lm[p - matchBase] = bl >= (uint32_t)kMinMatch ? (bl << 16) | (uint32_t)(pRel - (bestKey & 0x1FFFFu)) : 0u;
+        lm[p - matchBase] = bl >= kLongCap9 && room > kLongCap9 ? kLmUnknown << 16
+                            : bl >= (uint32_t)kMinMatch ? (bl << 16) | (uint32_t)(pRel - (bestKey & 0x1FFFFu)) : 0u;
       }
     }
     __syncthreads();
+    SZ4_D6(7);
   }
   }
   __threadfence_block();
   __syncthreads();
 
+  SZ4_D6(4);
   // 3. prefix maximum in text order.  Per target: E (exact: pass 1 finished it) resets the state to
   //    its own key, U (unknown: a pass-1 long match, or LM at the cap) invalidates it, B (big) takes
   //    the maximum of the state and its LM.  16 wavefronts take consecutive ranges; a range's carry-in
@@ -2707,8 +2844,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     }
     const uint32_t v = lm[idx];
     const uint32_t vl = v >> 16;
-    const uint32_t room = (uint32_t)(stopAbs - p);
-    if (vl >= kLongCap9 && room > kLongCap9) {
+    if (vl == kLmUnknown) {
       kind = 2;
       return;
     }
@@ -2769,14 +2905,18 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         valid = cValid;
       }
       anyHead |= __ballot(inR && kind != 0u) != 0;
+      bool rmq = false;
       if (phase == 1 && inR && kind == 0u && valid) {
         const uint64_t p = S.s0 + i, idx = p - matchBase;
         const uint32_t len = (uint32_t)(v >> 16) > i ? (uint32_t)(v >> 16) - i : 0u;
         const bool m = v != 0ull && len >= (uint32_t)kMinMatch;
+        const uint32_t d = 0xFFFFu - (uint32_t)(v & 0xFFFFu);
         mlen[idx] = m ? len : 0u;
-        mdist[idx] = m ? (uint16_t)(0xFFFFu - (uint32_t)(v & 0xFFFFu)) : (uint16_t)0;
+        mdist[idx] = m ? (uint16_t)d : (uint16_t)0;
         atomicAnd(&longBits[idx >> 5], ~(1u << (idx & 31)));
+        rmq = m && len >= kRmqLen && !(d == 1u && len >= kSameLetter);  // (a run target's exact length)
       }
+      if (__ballot(rmq) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
       // carry to the next 64: the last lane in range
       const uint32_t last = (r1 - i0 < 64u ? r1 - i0 : 64u) - 1u;
       cKey = ((uint64_t)rdlane((uint32_t)(v >> 32), last) << 32) | rdlane((uint32_t)v, last);
@@ -4991,8 +5131,8 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       hipFuncSetAttribute((const void*)k_find_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
-          hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, resolve);
+          hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
@@ -5012,8 +5152,8 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
       hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
-          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, resolve);
+          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
       hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
