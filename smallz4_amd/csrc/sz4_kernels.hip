@@ -2419,15 +2419,28 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   SZ4_D6(1);
   for (uint32_t gi = 0; gi < ng; gi++) {
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
-    const uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
+    // the group's run key, if it has one (its first or last member's; other keys in the group are
+    // 16-bit hash collisions, handled one by one below)
+    uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
+    if (!run_key(gKey)) gKey = gload4(in, S.w0 + slot_pos(compact, small, gb - 1));
     if (tid == 0) s_mixed = 0;
     __syncthreads();
     if (run_key(gKey)) {
+      uint32_t other = 0;
       for (uint32_t s = ga + tid; s < gb; s += kFindThreads)
-        if (src.ld4(S.w0 + slot_pos(compact, small, s)) != gKey) s_mixed = 1;
+        other += src.ld4(S.w0 + slot_pos(compact, small, s)) != gKey ? 1u : 0u;
+      if (other) atomicAdd(&s_mixed, other);
       __syncthreads();
+#if SZ4_DIAG == 6
+      if (tid == 0 && s_mixed) SZ4_D6C(17, 1);
+#endif
     }
-    if (run_key(gKey) && !s_mixed) {
+    // (a group of mostly other keys goes to the class path)
+    const bool runGroup = run_key(gKey) && s_mixed * 4u <= gb - ga;
+    __syncthreads();
+    if (tid == 0) s_mixed = 0;
+    __syncthreads();
+    if (runGroup) {
       // ---- a run-key group: its members are the chain positions with at
       // least 4 bytes of a run of v left.  A "piece" is a maximal stretch of consecutive member
       // positions: a whole run, or the part of one before / after the positions the same-letter
@@ -2441,13 +2454,20 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       SZ4_D6(6);
       if (tid == 0) SZ4_D6C(14, 1);
       // A. pieces: a member whose predecessor position is not a member starts one (block-wide scan);
-      //    C[ga + k] = its first, T[ga + k] = its first slot; a target member keeps its piece in lm
+      //    C[ga + k] = its first, T[ga + k] = its first slot; a target member keeps its piece in lm.
+      //    Members of other keys (collisions) are skipped.
+      auto is_run = [&](uint32_t t) { return src.ld4(S.w0 + slot_pos(compact, small, t)) == gKey; };
       uint32_t base = 0;
       for (uint32_t t0 = ga; t0 < gb; t0 += kFindThreads) {
         const uint32_t s = t0 + tid;
-        const bool inG = s < gb;
+        const bool inG = s < gb && is_run(s);
         const uint32_t r = inG ? slot_pos(compact, small, s) : 0u;
-        const bool first = inG && (s == ga || slot_pos(compact, small, s - 1) + 1u != r);
+        bool first = inG;
+        if (inG) {
+          int32_t t = (int32_t)s - 1;
+          while (t >= (int32_t)ga && !is_run((uint32_t)t)) t--;
+          first = t < (int32_t)ga || slot_pos(compact, small, (uint32_t)t) + 1u != r;
+        }
         uint32_t tot = 0;
         const uint32_t k = base + block_excl_scan(first ? 1u : 0u, s_wsum, &tot);
         if (first) {
@@ -2479,7 +2499,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         }
         __syncthreads();
         if (k < nRuns) {
-          const uint32_t lastRel = r + (sNext - 1u - sFirst);
+          uint32_t tl = sNext - 1u;  // the piece's last member: the last run member before the next piece
+          while (tl > sFirst && !is_run(tl)) tl--;
+          const uint32_t lastRel = slot_pos(compact, small, tl);
           uint64_t e = S.w0 + lastRel + 4;
           uint32_t kind = 0, extra = 0;
           if ((src.ld4(e) & 0xFFu) == v) {
@@ -2504,6 +2526,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         __syncthreads();
       }
       if (bad) s_mixed = 1;
+#if SZ4_DIAG == 6
+      if (bad) SZ4_D6C(16, 1);
+#endif
       __threadfence_block();
       __syncthreads();
       //    the piece at the window's end: its run's end by wave 0, 256 bytes per step, jumping intervals
@@ -2541,6 +2566,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       __syncthreads();
       SZ4_D6(2);
       if (tid == 0) SZ4_D6C(12, nRuns);
+#if SZ4_DIAG == 6
+      if (tid == 0 && !s_mixed && nRuns > (uint32_t)(S.s1 - S.s0)) SZ4_D6C(18, 1);
+#endif
       if (!s_mixed && nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
       // B. buckets by next byte
       for (uint32_t k = tid; k < nRuns; k += kFindThreads) atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u);
@@ -2581,7 +2609,10 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t s = ga + item * 64 + lane;
         const uint32_t pRel = s < gb ? slot_pos(compact, small, s) : 0u;
         const uint64_t p = S.w0 + pRel;
-        const bool act = s < gb && is_target(p);
+        const bool tgt = s < gb && is_target(p);
+        const uint32_t pKey = tgt ? src.ld4(p) : 0u;
+        const bool coll = tgt && pKey != gKey;  // a collision member: searched one by one, below
+        const bool act = tgt && !coll;
         const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its piece
         if (act) SZ4_D6C(8, 1);
         uint32_t fi = 0, eiRel = 0, li = 0;
@@ -2589,7 +2620,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t ai = act ? C[ga + lo] >> 17 : 0u;
         const uint64_t ei = S.w0 + eiRel;  // p's run ends here
         const uint32_t R = act ? eiRel - pRel : 0u;
-        const uint32_t room = act ? (uint32_t)(stopAbs - p) : 0u;
+        const uint32_t room = tgt ? (uint32_t)(stopAbs - p) : 0u;
         const uint32_t limit = room;  // exact lengths (no pass-1 cap; the result goes to mlen, u32)
         const uint32_t lbRel = p > S.w0 + kWindow ? (uint32_t)(p - kWindow - S.w0) : 0u;
         uint32_t bl = 0, bc = 0;  // best length, its candidate (rel)
@@ -2679,7 +2710,37 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           }
           if (lane == t) offer((uint32_t)(best >> 17), (uint32_t)(best & 0x1FFFFu));
         }
-        if (act) {
+        // collision members: every group member of the same key below, by the whole wavefront
+        uint64_t cm = __ballot(coll);
+        while (cm) {
+          const uint32_t t = (uint32_t)__builtin_ctzll(cm);
+          cm &= cm - 1;
+          const uint32_t st = rdlane(s, t), pr = rdlane(pRel, t), kt = rdlane(pKey, t);
+          const uint32_t rm = rdlane(room, t), lb = rdlane(lbRel, t);
+          uint64_t best = 0;
+          for (uint32_t b0 = ga; b0 < st; b0 += 64) {
+            const uint32_t cs = b0 + lane;
+            const uint32_t cr = cs < st ? slot_pos(compact, small, cs) : 0u;
+            uint32_t l = 0;
+            if (cs < st && cr >= lb && cr < pr && src.ld4(S.w0 + cr) == kt) {
+              l = 4;
+              while (l < rm) {
+                const uint32_t x = src.ld4(S.w0 + pr + l) ^ src.ld4(S.w0 + cr + l);
+                if (x) {
+                  l += (uint32_t)__builtin_ctz(x) >> 3;
+                  break;
+                }
+                l += 4;
+              }
+              l = l < rm ? l : rm;
+            }
+            const uint64_t key = l ? ((uint64_t)l << 17) | cr : 0ull;
+            const uint64_t wm = wave_max_u64(key);
+            best = wm > best ? wm : best;
+          }
+          if (lane == t) offer((uint32_t)(best >> 17), (uint32_t)(best & 0x1FFFFu));
+        }
+        if (tgt) {
           // final: pass 1 and the prefix maximum below read it as an exact target
           const uint64_t idx = p - matchBase;
           const bool m = bl >= (uint32_t)kMinMatch;
