@@ -93,6 +93,16 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
   return v;
 }
 
+__device__ __forceinline__ int32_t wave_max_i32(int32_t v)
+{
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const int32_t o = __shfl_xor(v, m, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
 #pragma unroll
@@ -2455,12 +2465,24 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       if (tid == 0) SZ4_D6C(14, 1);
       // A. pieces: a member whose predecessor position is not a member starts one (block-wide scan);
       //    C[ga + k] = its first, T[ga + k] = its first slot; a target member keeps its piece in lm.
-      //    Members of other keys (collisions) are skipped.
+      //    Members of other keys (hash collisions) go to a list of their own, in position order from
+      //    the top: C[gb - 1 - j] = the j-th one (rel); a target among them keeps its j in lm.
       auto is_run = [&](uint32_t t) { return src.ld4(S.w0 + slot_pos(compact, small, t)) == gKey; };
-      uint32_t base = 0;
+      uint32_t base = 0, nColl = 0;
       for (uint32_t t0 = ga; t0 < gb; t0 += kFindThreads) {
         const uint32_t s = t0 + tid;
         const bool inG = s < gb && is_run(s);
+        const bool isColl = s < gb && !inG;
+        {
+          uint32_t tc = 0;
+          const uint32_t j = nColl + block_excl_scan(isColl ? 1u : 0u, s_wsum, &tc);
+          if (isColl) {
+            const uint32_t rc = slot_pos(compact, small, s);
+            C[gb - 1u - j] = rc;
+            if (is_target(S.w0 + rc)) lm[S.w0 + rc - matchBase] = j;
+          }
+          nColl += tc;
+        }
         const uint32_t r = inG ? slot_pos(compact, small, s) : 0u;
         bool first = inG;
         if (inG) {
@@ -2613,7 +2635,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t pKey = tgt ? src.ld4(p) : 0u;
         const bool coll = tgt && pKey != gKey;  // a collision member: searched one by one, below
         const bool act = tgt && !coll;
-        const uint32_t lo = act ? lm[p - matchBase] : 0u;  // its piece
+        const uint32_t lo = tgt ? lm[p - matchBase] : 0u;  // its piece (a collision member: its list index)
         if (act) SZ4_D6C(8, 1);
         uint32_t fi = 0, eiRel = 0, li = 0;
         if (act) piece(lo, fi, eiRel, li);
@@ -2645,6 +2667,16 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             offer(Rp + ext_len(S.w0 + ej, ei, limit - Rp), c);
           }
         };
+#if SZ4_DIAG == 6
+        uint64_t w6 = __builtin_readcyclecounter();
+        auto W6 = [&](int k) {
+          const uint64_t now = __builtin_readcyclecounter();
+          if (lane == 0) SZ4_D6C(k, now - w6);
+          w6 = now;
+        };
+#else
+        auto W6 = [&](int) {};
+#endif
         const uint32_t need = R < limit ? R : limit;
         int32_t wj = -1;       // a piece start's walk: next piece to look at when still open
         bool open = false;
@@ -2681,6 +2713,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             wj--;
           }
         }
+        W6(21);
         // ... and the rare long walks by the whole wavefront, 64 pieces per step
         uint64_t pend = __ballot(open);
         while (pend) {
@@ -2710,19 +2743,22 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           }
           if (lane == t) offer((uint32_t)(best >> 17), (uint32_t)(best & 0x1FFFFu));
         }
-        // collision members: every group member of the same key below, by the whole wavefront
+        W6(22);
+        // collision members: the list entries of the same key below, by the whole wavefront
         uint64_t cm = __ballot(coll);
         while (cm) {
           const uint32_t t = (uint32_t)__builtin_ctzll(cm);
           cm &= cm - 1;
-          const uint32_t st = rdlane(s, t), pr = rdlane(pRel, t), kt = rdlane(pKey, t);
+          if (lane == 0) SZ4_D6C(19, 1);
+          const uint32_t jt = rdlane(lo, t), pr = rdlane(pRel, t), kt = rdlane(pKey, t);
           const uint32_t rm = rdlane(room, t), lb = rdlane(lbRel, t);
           uint64_t best = 0;
-          for (uint32_t b0 = ga; b0 < st; b0 += 64) {
-            const uint32_t cs = b0 + lane;
-            const uint32_t cr = cs < st ? slot_pos(compact, small, cs) : 0u;
+          for (uint32_t b0 = 0; b0 < jt; b0 += 64) {  // the list entries below it
+            if (lane == 0) SZ4_D6C(20, 1);
+            const uint32_t j = b0 + lane;
+            const uint32_t cr = j < jt ? C[gb - 1u - j] : 0u;
             uint32_t l = 0;
-            if (cs < st && cr >= lb && cr < pr && src.ld4(S.w0 + cr) == kt) {
+            if (j < jt && cr >= lb && src.ld4(S.w0 + cr) == kt) {
               l = 4;
               while (l < rm) {
                 const uint32_t x = src.ld4(S.w0 + pr + l) ^ src.ld4(S.w0 + cr + l);
@@ -2740,6 +2776,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           }
           if (lane == t) offer((uint32_t)(best >> 17), (uint32_t)(best & 0x1FFFFu));
         }
+        W6(23);
         if (tgt) {
           // final: pass 1 and the prefix maximum below read it as an exact target
           const uint64_t idx = p - matchBase;
@@ -4231,6 +4268,10 @@ __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec_rmq(SZ4_DP_SPEC_ARG
 // only enters the offset tables; the others get their speculative values back and are repaired
 // serially as before.
 constexpr uint32_t kDpSide = 512;
+// range-minimum blocks: k_dp_fix<true> also saves the UP/DOWN keys it overwrites, down to the bottom
+// of its convergence point's rmq block (kDpSide + 255 positions at most), after the cost side
+constexpr uint32_t kDpSideKeys = kDpSide + 256;
+constexpr uint32_t kDpSideStride = kDpSide + kDpSideKeys;
 
 template <bool kPar>
 __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
@@ -4252,7 +4293,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   if constexpr (kPar) {
     if (blockIdx.x >= ndp) return;
     const DpSeg G0 = dpSegs[blockIdx.x];
-    if (G0.k == 0 || (longFlag[G0.block] & kFlagRmq)) return;
+    if (G0.k == 0) return;
     bIdx = G0.block;
     kFirst = G0.k;
     kEnd = G0.k + 1;
@@ -4280,7 +4321,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   uint32_t* S = sel + base;
   const uint32_t first = dpSegs[B.dpFirst].hi;  // n - 6: the last parsed position
   const int32_t top = (int32_t)first;
-  const bool rmq = kPar ? false : (longFlag[bIdx] & kFlagRmq) != 0u;
+  const bool rmq = (longFlag[bIdx] & kFlagRmq) != 0u;
   uint32_t* up = upAll + base;
   uint32_t* down = downAll + base;
   if (!kPar && lane == 0) {
@@ -4292,9 +4333,11 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   __syncthreads();
   // exact cost of a position above the segment being repaired (0 past the parsed range); k_dp_fix<true>
   // takes the stored (speculative) costs, exact up to one offset where its result is used
+  int32_t readTop = 0, keyTop = -1;  // k_dp_fix<true>: highest position above the segment read (costs, keys)
   auto exact_above = [&](uint32_t j) -> uint32_t {
     if (j > first) return 0u;
     if constexpr (kPar) {
+      readTop = (int32_t)j > readTop ? (int32_t)j : readTop;
       return cost[j];
     } else {
       const uint32_t k = (first - j) / B.dpSize;
@@ -4303,7 +4346,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     }
   };
   // k_dp_fix<false> over blocks that k_dp_fix<true> repaired: the records 64 segments at a time
-  const bool par = !kPar && !rmq;
+  const bool par = !kPar;
+  uint32_t prevKeyLim = 0;  // convBlk of segment k - 1
   uint4 recV = make_uint4(0u, 0u, 0u, 0u);
   uint32_t prevV = 0, prevConv = 0;  // offset below segment k - 1's convergence point, that point
   bool prevDone = true;              // segment k - 1's repair converged (segment 0 is exact)
@@ -4321,27 +4365,38 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       const uint32_t rConv = rdlane(recV.x, t), rDelta = rdlane(recV.y, t);
       const uint32_t rReach = rdlane(recV.z, t), rFlag = rdlane(recV.w, t);
       recNoMatch = (rFlag & 2u) != 0u;
-      if ((rFlag & 1u) && (k == 1u || (prevDone && rReach < prevConv))) {
+      const uint32_t rKeyTop = rFlag >> 2;  // highest key position read + 1, 0: none
+      // the bottom of the rmq block of its convergence point: keys at and above it were rewritten
+      const uint32_t rKeyLim = rmq && (rFlag & 1u) ? max((uint32_t)rmq_block_top(top, (int32_t)rConv) - 255u, (uint32_t)lo)
+                                                   : rConv;
+      if ((rFlag & 1u) && (k == 1u || (prevDone && rReach < prevConv && (rKeyTop == 0u || rKeyTop - 1u < prevKeyLim)))) {
         // everything it read was exact - prevV: its costs are exact - prevV
         if (lane == 0) {
           convTab[k] = rConv;
-          convBlk[k] = rConv;
+          convBlk[k] = rKeyLim;
           aboveTab[k] = prevV;
           deltaTab[k] = prevV + rDelta;
         }
         prevV += rDelta;
         prevConv = rConv;
+        prevKeyLim = rKeyLim;
         prevDone = true;
         __syncthreads();
         continue;
       }
       // repaired from a wrong state: the speculative values back, then the serial repair
-      uint2* sd = side + (uint64_t)(B.dpFirst + k) * kDpSide;
+      uint2* sd = side + (uint64_t)(B.dpFirst + k) * kDpSideStride;
       for (int32_t t2 = (int32_t)lane; hi - t2 >= (int32_t)rConv; t2 += 64) {  // rConv = hi + 1: nothing written
         const uint2 v = sd[t2];
         cost[hi - t2] = v.x;
         S[hi - t2] = v.y;
       }
+      if (rmq)
+        for (int32_t t2 = (int32_t)lane; hi - t2 >= (int32_t)rKeyLim; t2 += 64) {
+          const uint2 v = sd[kDpSide + t2];
+          up[hi - t2] = v.x;
+          down[hi - t2] = v.y;
+        }
       // the stores complete before the reloads below; only this wavefront reads them (same CU), so a
       // workgroup-scope fence does -- __threadfence() would write back and invalidate the XCD's whole L2
       // (buffer_wbl2 sc1 + buffer_inv sc1 on gfx950) once per restored segment
@@ -4365,8 +4420,12 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     auto key_cost = [&](int32_t j, uint32_t key) -> uint32_t {
       uint32_t c = key >> 8;
       if (j > hi) {
-        const uint32_t kk = (first - (uint32_t)j) / B.dpSize;
-        if ((uint32_t)j < convBlk[kk]) c += deltaTab[kk];
+        if constexpr (kPar) {
+          keyTop = j > keyTop ? j : keyTop;
+        } else {
+          const uint32_t kk = (first - (uint32_t)j) / B.dpSize;
+          c += (uint32_t)j < convBlk[kk] ? deltaTab[kk] : aboveTab[kk];
+        }
       }
       return c;
     };
@@ -4409,7 +4468,11 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       const uint32_t cnt = (uint32_t)(h - cl + 1);
       if constexpr (kPar) {
         if ((uint32_t)(hi - h) >= kDpSide) break;  // gives up: k_dp_fix<false> repairs it
-        if (in) side[(uint64_t)blockIdx.x * kDpSide + (uint32_t)(hi - ip)] = make_uint2(cC, cS);
+        if (in) {
+          uint2* sd = side + (uint64_t)blockIdx.x * kDpSideStride;
+          sd[(uint32_t)(hi - ip)] = make_uint2(cC, cS);
+          if (rmq) sd[kDpSide + (uint32_t)(hi - ip)] = make_uint2(up[ip], down[ip]);
+        }
         lowW = cl;
       }
       if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
@@ -4582,6 +4645,10 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
           const int32_t jt = rmq_block_top(top, conv);
           const int32_t jb0 = jt - 255;
           const int32_t jb = jb0 > lo ? jb0 : lo;
+          if constexpr (kPar) {  // the keys below the chunks it went through: saved before rewritten
+            uint2* sd = side + (uint64_t)blockIdx.x * kDpSideStride + kDpSide;
+            for (int32_t j = jb + (int32_t)lane; j < lowW; j += 64) sd[(uint32_t)(hi - j)] = make_uint2(up[j], down[j]);
+          }
           auto exact = [&](int32_t j) -> uint32_t {
             return j >= conv ? ring[j & (kRing - 1)] : ld_fresh(&cost[j]) + convDelta;
           };
@@ -4592,8 +4659,10 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       }
     }
     if constexpr (kPar) {
+      const int32_t rd = wave_max_i32(readTop > maxReach ? readTop : maxReach);
+      const uint32_t kt = (uint32_t)(wave_max_i32(keyTop) + 1);
       if (lane == 0)
-        dpRec[blockIdx.x] = make_uint4(done ? (uint32_t)conv : (uint32_t)lowW, convDelta, (uint32_t)maxReach, done ? 1u : 0u);
+        dpRec[blockIdx.x] = make_uint4(done ? (uint32_t)conv : (uint32_t)lowW, convDelta, (uint32_t)rd, (done ? 1u : 0u) | kt << 2);
     } else {
       if (lane == 0) {
         if (!done || !rmq) convBlk[k] = (uint32_t)conv;
@@ -4607,6 +4676,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       prevConv = (uint32_t)conv;
       prevDone = done;
       __syncthreads();
+      prevKeyLim = convBlk[k];
     }
   }
 }
@@ -5162,7 +5232,7 @@ void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const B
   if (nsegs) hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB);
 }
 
-uint32_t dp_side_positions() { return kDpSide; }
+uint32_t dp_side_positions() { return kDpSideStride; }
 
 uint32_t find_lds_bytes() { return 65536 + 16; }
 uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
