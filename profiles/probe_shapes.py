@@ -29,6 +29,7 @@ KINDS = {
     "image": lambda n, rng: synth._image16(n, rng),
     "src": lambda n, rng: synth._source(n, rng),
     "silesia": lambda n, rng: synth.silesia_like(n, seed=2),
+    "zu": lambda n, rng: synth.zeros_urandom_range(0, n, seed=10),
 }
 
 

@@ -103,6 +103,26 @@ __device__ __forceinline__ int32_t wave_max_i32(int32_t v)
   return v;
 }
 
+// clears bit idx of `bits` for the lanes where `pred` holds: one atomic per distinct word (lanes with
+// nearby indices share words; 64 atomics on one address serialise in L2)
+__device__ __forceinline__ void wave_clear_bits(uint32_t* bits, uint64_t idx, bool pred)
+{
+  uint64_t rest = __ballot(pred);
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint64_t w = idx >> 5;
+  while (rest) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(rest);
+    const uint64_t wl = ((uint64_t)__builtin_amdgcn_readlane((int)(w >> 32), l) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w, l);
+    const bool mine = pred && w == wl;
+    uint32_t m = mine ? 1u << (idx & 31) : 0u;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) m |= (uint32_t)__shfl_xor((int)m, d, 64);
+    if (lane == l) atomicAnd(&bits[wl], ~m);
+    rest &= ~__ballot(mine);
+  }
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
 {
 #pragma unroll
@@ -707,8 +727,14 @@ constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_big / k_find_long9
 constexpr uint32_t kBigRun = 2048;    // the same for a run key (vvvv) in blocks k_find_big takes
-constexpr uint32_t kBigRunL = 32;     // ... in blocks above 64 KiB (k_find_big's run table is exact and cheap)
-constexpr uint32_t kLpfMin = 256;     // ... and for an LPF target (below)
+#ifndef SZ4_BIG_RUN_L
+#define SZ4_BIG_RUN_L 32
+#endif
+#ifndef SZ4_LPF_MIN
+#define SZ4_LPF_MIN 256
+#endif
+constexpr uint32_t kBigRunL = SZ4_BIG_RUN_L;  // ... in blocks above 64 KiB (k_find_big's run table is exact and cheap)
+constexpr uint32_t kLpfMin = SZ4_LPF_MIN;     // ... and for an LPF target (below)
 constexpr uint32_t kLpfProbe = 8;
 __device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
 constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
@@ -2608,7 +2634,25 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         }
       }
       __syncthreads();
-      for (uint32_t k = tid; k < nRuns; k += kFindThreads) BK[atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u)] = k;
+      // (in piece order inside a bucket: one wavefront, 64 pieces at a time, one counter update per
+      // distinct byte)
+      if (wave == 0) {
+        const uint64_t below = (1ull << lane) - 1ull;
+        for (uint32_t k0 = 0; k0 < nRuns; k0 += 64) {
+          const uint32_t k = k0 + lane;
+          const uint32_t a = k < nRuns ? C[ga + k] >> 17 : 0xFFFFFFFFu;
+          uint64_t rest = __ballot(k < nRuns);
+          while (rest) {
+            const uint32_t l = (uint32_t)__builtin_ctzll(rest);
+            const uint32_t al = rdlane(a, l);
+            const uint64_t m = __ballot(a == al);
+            const uint32_t at = s_cur[0][al];
+            if (a == al) BK[at + (uint32_t)__builtin_popcountll(m & below)] = k;
+            if (lane == 0) s_cur[0][al] = at + (uint32_t)__builtin_popcountll(m);
+            rest &= ~m;
+          }
+        }
+      }
       __threadfence_block();
       __syncthreads();
       // a piece's first, run end and last member (rel)
@@ -2654,17 +2698,26 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         };
         // the pieces before p's that hold a position with exactly R bytes of v left (R(c) = R(p)), and
         // whose run is followed by the same byte: R bytes + the common prefix after the two runs
+        //   (the bucket is in piece order: from p's own piece down, nearest first, to the window's start)
         auto same_r = [&](uint32_t Rp) {
           if (Rp >= limit || ai == kAEnd) return;
-          for (uint32_t b = s_cls[ai]; b < s_cls[ai + 1]; b++) {
+          const uint32_t b0 = s_cls[ai];
+          uint32_t bLo = b0, bHi = s_cls[ai + 1];  // p's piece in it
+          while (bLo < bHi) {
+            const uint32_t mid = (bLo + bHi) >> 1;
+            if (BK[mid] < lo) bLo = mid + 1;
+            else bHi = mid;
+          }
+          for (uint32_t b = bLo; b-- > b0;) {
             SZ4_D6C(9, 1);
-            const uint32_t j = BK[b];
-            if (j >= lo) continue;
             uint32_t fj, ej, lj;
-            piece(j, fj, ej, lj);
+            piece(BK[b], fj, ej, lj);
+            if (lj < lbRel) break;     // it and every earlier piece lie below the window
             const uint32_t c = ej - Rp;  // its position with R(c) = Rp
             if (c < fj || c > lj || c < lbRel) continue;
-            offer(Rp + ext_len(S.w0 + ej, ei, limit - Rp), c);
+            const uint32_t l = Rp + ext_len(S.w0 + ej, ei, limit - Rp);
+            offer(l, c);
+            if (l >= limit) break;  // the longest there is; the nearer ones came first
           }
         };
 #if SZ4_DIAG == 6
@@ -2783,9 +2836,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           const bool m = bl >= (uint32_t)kMinMatch;
           mlen[idx] = m ? bl : 0u;
           mdist[idx] = m ? (uint16_t)(pRel - bc) : (uint16_t)0;
-          atomicAnd(&longBits[idx >> 5], ~(1u << (idx & 31)));
           rmq |= m && bl >= kRmqLen && !(pRel - bc == 1u && bl >= kSameLetter);
         }
+        wave_clear_bits(longBits, p - matchBase, tgt);
       }
       if (__ballot(rmq) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
       __syncthreads();
@@ -3011,9 +3064,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         const uint32_t d = 0xFFFFu - (uint32_t)(v & 0xFFFFu);
         mlen[idx] = m ? len : 0u;
         mdist[idx] = m ? (uint16_t)d : (uint16_t)0;
-        atomicAnd(&longBits[idx >> 5], ~(1u << (idx & 31)));
         rmq = m && len >= kRmqLen && !(d == 1u && len >= kSameLetter);  // (a run target's exact length)
       }
+      wave_clear_bits(longBits, S.s0 + i - matchBase, phase == 1 && inR && kind == 0u && valid);
       if (__ballot(rmq) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
       // carry to the next 64: the last lane in range
       const uint32_t last = (r1 - i0 < 64u ? r1 - i0 : 64u) - 1u;
