@@ -64,7 +64,7 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
  * Any n in bounded memory: the blocks are compressed in pieces of at most
- * sz4_set_batch_chunk bytes (128 MiB by default, ~10 GB of scratch).
+ * sz4_set_batch_chunk bytes (256 MiB by default, ~19 GB of scratch).
  *
  *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
  *   block_size    1 .. 4 MiB
@@ -119,7 +119,7 @@ int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_by
 void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
- * device scratch is about 60-75 bytes per piece byte.  0 restores the 128 MiB default. */
+ * device scratch is about 60-75 bytes per piece byte.  0 restores the 256 MiB default. */
 void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured

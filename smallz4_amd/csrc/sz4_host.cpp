@@ -136,7 +136,7 @@ struct sz4_ctx {
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
-  uint64_t batchChunk = 128ull << 20;  // sz4_compress_blocks_device: input bytes per internal pipeline run
+  uint64_t batchChunk = 256ull << 20;  // sz4_compress_blocks_device: input bytes per internal pipeline run
   bool batchChunked = false;           // the last sz4_compress_blocks_device call ran in several pieces
   uint64_t streamPlanKey[5] = {~0ull, 0, 0, 0, 0};  // stream path: the chunk shape the current plan is for
   // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
@@ -1190,7 +1190,7 @@ void sz4_set_stream_chunk(sz4_ctx* c, uint64_t bytes)
 
 void sz4_set_batch_chunk(sz4_ctx* c, uint64_t bytes)
 {
-  if (c) c->batchChunk = bytes ? bytes : (128ull << 20);
+  if (c) c->batchChunk = bytes ? bytes : (256ull << 20);
 }
 
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)

@@ -78,13 +78,13 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     # HBM footprint of the context for this slice (grow-only scratch)
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
-    # bounded: sz4_compress_blocks_device runs 128 MiB pieces (~60-75 B of scratch per piece byte)
-    assert footprint < 16 << 30
+    # bounded: sz4_compress_blocks_device runs 256 MiB pieces (~60-75 B of scratch per piece byte)
+    assert footprint < 24 << 30
 
 
 def test_batch_4gib_one_call_bounded_memory(compressor):
     """4 GiB of configs[4]'s shape (zeros/urandom runs, 256 KiB blocks) in ONE sz4_compress_blocks_device
-    call: the context's scratch stays under 16 GiB (the call runs 128 MiB pieces), the frame decodes
+    call: the context's scratch stays under 24 GiB (the call runs 256 MiB pieces), the frame decodes
     back on the device, every size word walks, and sampled blocks equal the oracle's."""
     import torch
     bs = 262144
@@ -97,7 +97,7 @@ def test_batch_4gib_one_call_bounded_memory(compressor):
     size = compressor.compress_blocks_device(t.data_ptr(), len(data), out.data_ptr(), cap, bs, 65535, "none", stream)
     footprint = compressor.device_bytes()
     print(f"4 GiB in one call: context holds {footprint / 2**30:.2f} GiB")
-    assert footprint < 16 << 30
+    assert footprint < 24 << 30
     # round trip on the device
     fr = torch.empty(size + 11, dtype=torch.uint8, device="cuda")
     fr[:7] = torch.tensor(list(shard.HEADER), dtype=torch.uint8)
