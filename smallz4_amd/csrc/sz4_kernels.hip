@@ -1404,7 +1404,10 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     // target pass 2's seed: the nearest candidate at the cap), appended to its tile's bucket
     {
       const uint32_t rel = active ? (uint32_t)(p - S.s0) : 0u;
-      const uint32_t packed = ((isLong ? kOutLong : (bestDist ? bestLen : 0u)) << 16) | (big ? 0u : (bestDist & 0xFFFFu));
+      // a run-key target whose match reached the cap goes to k_find_big as well (blocks above 64 KiB):
+      // its run table gives the exact length, where pass 2 would compare the whole run per candidate
+      const bool lateBig = unlimited && cut == kNone && active && isLong && !big && lpfOk && lpfBlock && run_key(me0);
+      const uint32_t packed = ((isLong ? kOutLong : (bestDist ? bestLen : 0u)) << 16) | (big || lateBig ? 0u : (bestDist & 0xFFFFu));
 #pragma unroll
       for (uint32_t k = 0; k < kOutTiles; k++) {
         const uint64_t m = __ballot(active && (rel >> kOutTileBits) == k);
@@ -2044,6 +2047,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
         if (src.ld4(c) == key) {
           const uint32_t need = bestDist == 0u ? 4u : (dist < bestDist ? bestLen : bestLen + 1u);
           const uint32_t got = prefix_if_at_least(src, p, c, need < 4u ? 4u : need, room);
+#if SZ4_DIAG == 5
+          atomicAdd((unsigned long long*)&sz4_diag[7], (unsigned long long)((need > got ? need : got) / 4u + 1u));
+#endif
           if (got >= need && got != 0u && (got > bestLen || dist < bestDist)) {
             bestLen = got;
             bestDist = dist;
@@ -2144,6 +2150,22 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     const uint32_t p1 = lane < cnt ? mlen[myIdx] : 0u;
     if (__ballot(p1 == kLongMatch) == 0) continue;
     const bool lg = lane < cnt && long_bit(p);
+#if SZ4_DIAG == 5
+    {
+      const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(lane < cnt && p1 == kLongMatch && lg));
+      const uint32_t ni = (uint32_t)__builtin_popcountll(__ballot(lane < cnt && p1 == kLongMatch && !lg));
+      if (lane == 0 && nl) atomicAdd((unsigned long long*)&sz4_diag[5], (unsigned long long)nl);
+      if (lane == 0 && ni) atomicAdd((unsigned long long*)&sz4_diag[6], (unsigned long long)ni);
+      if (lane < cnt && p1 == kLongMatch && lg) {
+        const uint64_t k = atomicAdd((unsigned long long*)&sz4_diag[15], 1ull);
+        if (k < 512) {
+          sz4_diag[64 + 3 * k] = p - B.start;
+          sz4_diag[65 + 3 * k] = src.ld4(p) | ((uint64_t)src.ld4(p + 4) << 32);
+          sz4_diag[66 + 3 * k] = (uint64_t)mdist[myIdx] | ((uint64_t)(B.end - B.start) << 32);
+        }
+      }
+    }
+#endif
     // marked but never sorted: shortcut-interval targets copy the predecessor's match, minus one
     if (lane < cnt && p1 == kLongMatch && !lg) {
       for (uint32_t k = 0; k < niv; k++)
@@ -2407,6 +2429,10 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     }
     __syncthreads();
   }
+#if SZ4_DIAG == 6
+  if (tid == 0 && ng == 0) SZ4_D6C(24, 1);
+  if (tid == 0 && ng > kMaxBigGroups) SZ4_D6C(25, 1);
+#endif
   if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
   const uint64_t stopAbs = B.end - kTailLiterals;
 
@@ -3057,6 +3083,14 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       }
       anyHead |= __ballot(inR && kind != 0u) != 0;
       bool rmq = false;
+#if SZ4_DIAG == 6
+      if (phase == 1 && resolveOnly) {
+        const uint32_t nb = (uint32_t)__builtin_popcountll(__ballot(inR && kind == 0u && !valid));
+        if (lane == 0 && nb) SZ4_D6C(26, nb);
+        const uint32_t nu = (uint32_t)__builtin_popcountll(__ballot(inR && kind == 2u));
+        if (lane == 0 && nu) SZ4_D6C(27, nu);
+      }
+#endif
       if (phase == 1 && inR && kind == 0u && valid) {
         const uint64_t p = S.s0 + i, idx = p - matchBase;
         const uint32_t len = (uint32_t)(v >> 16) > i ? (uint32_t)(v >> 16) - i : 0u;

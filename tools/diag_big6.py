@@ -25,9 +25,9 @@ comp.compress_blocks(data[:bs * 4], bs, 65535)
 lib.sz4_diag_clear()
 comp.set_timing(True)
 comp.compress_blocks(data, bs, 65535)
-buf = np.zeros(24, dtype=np.uint64)
-lib.sz4_diag_read(buf.ctypes.data, 24)
+buf = np.zeros(28, dtype=np.uint64)
+lib.sz4_diag_read(buf.ctypes.data, 28)
 names = ["detect", "window", "A", "A2scan", "phase3_wait", "C_run", "loop_top", "class_path", "run_targets",
          "bucket_it", "walk_it", "coop_steps", "pieces", "class_groups", "run_groups", "segments", "bad_threads", "mixed", "too_many_runs",
-         "coll_targets", "coll_steps", "w_local", "w_coop", "w_coll"]
+         "coll_targets", "coll_steps", "w_local", "w_coop", "w_coll", "ng0", "ng_over", "B_unresolved", "U_left"]
 print(kind, mb, bs, {k: int(v) for k, v in zip(names, buf)}, {k: round(v, 2) for k, v in comp.last_stage_ms().items()})

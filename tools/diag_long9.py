@@ -23,7 +23,11 @@ lib.sz4_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
 lib.sz4_diag_clear()
 comp.set_timing(True)
 comp.compress_blocks(data, 262144, 65535)
-buf = np.zeros(8, dtype=np.uint64)
-lib.sz4_diag_read(buf.ctypes.data, 8)
-print(mb, "MB", dict(zip(["best_of", "of_steps", "best_lane", "lane_steps", "rewalks"], [int(x) for x in buf[:5]])),
+buf = np.zeros(64 + 3 * 512, dtype=np.uint64)
+lib.sz4_diag_read(buf.ctypes.data, len(buf))
+print(mb, "MB", dict(zip(["best_of", "of_steps", "best_lane", "lane_steps", "rewalks", "marked", "interval", "cmp_words"], [int(x) for x in buf[:8]])),
       comp.last_stage_ms())
+if len(sys.argv) > 2:
+    for k in range(min(512, int(buf[15]))):
+        rel, w, md = int(buf[64 + 3 * k]), int(buf[65 + 3 * k]), int(buf[66 + 3 * k])
+        print(rel, f"{w:016x}", md & 0xFFFF, md >> 32)
