@@ -1,0 +1,443 @@
+// sz4_dict.hip -- dictionary mode on the whole GPU (smallz4.h:544-571 prepends the dictionary, the
+// match loop at smallz4.h:603-760 is the usual one).
+//
+// With a dictionary every block starts at 65535 mod 65536, so the reference writes a chain entry at
+// the block-relative slot i & 65535 (smallz4.h:656) and reads it back at the absolute slot
+// pos & 65535 (smallz4.h:190, 200, 694): a read finds the entry of the neighbouring position, and the
+// chains stop being runs of one key.  They are still a pure function of the insertion order:
+//   * previousHash of an inserted position is the distance to the last earlier inserted position with
+//     the same getHash32 (smallz4.h:648-666) -- a sort by (hash, position);
+//   * the value a read of slot s sees at insertion step t is the one the latest insertion at or
+//     before t with block-relative index == s (mod 65536) wrote (read_slot below): O(1) per read, from
+//     the arrays of every position's previousHash / previousExact;
+//   * previousExact (smallz4.h:668-720) is the hash-chain walk over those snapshot reads, and
+//     findLongestMatch (smallz4.h:173-255) the exact-chain walk over them: one lane per position.
+// The same-letter shortcut (smallz4.h:631-643) would make the set of inserted positions depend on the
+// matches; it needs a distance-1 match longer than MaxSameLetter, i.e. a run of more than 65 300 equal
+// bytes inside a block.  k_dict_detect flags a chunk that has a uniform aligned 32 KiB window inside
+// its blocks (a superset of those runs) and such a chunk takes the reference loop replayed in order
+// (k_dict_matches in sz4_kernels.hip), as do legacy frames.
+//
+//   k_dict_begin    the carried tables: reset (first chunk) or shifted with the staged coordinates
+//   k_dict_detect   the fallback gate above
+//   k_dict_keys     per block: (hash << 23 | position) of its own insertions and the 64 KiB before them
+//   (rocPRIM radix sort of the keys)
+//   k_dict_ph       previousHash of every insertion: its predecessor in the sorted run of its hash
+//   k_dict_last     the hash table's final positions (lastHash, smallz4.h:650-652)
+//   k_dict_pe       previousExact of every insertion: the hash-chain walk over snapshot reads
+//   k_dict_search   findLongestMatch of every linked position of every block
+//   k_dict_skip     greedy/lazy levels: the reference's skip bookkeeping (smallz4.h:726-744), per block
+//   k_dict_carry    the final chain tables, for the next chunk
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "sz4_device.h"
+#include "sz4_internal.h"
+
+namespace sz4 {
+
+constexpr uint32_t kDictNoPos = 0xFFFFFFFFu;
+constexpr uint32_t kDictPosBits = 23;  // a block's insertions and the 64 KiB below them: < 2^23 positions
+constexpr uint64_t kDictPosMask = (1ull << kDictPosBits) - 1;
+constexpr uint32_t kDictRmqLen = 274;  // as kRmqLen in sz4_kernels.hip: the parse's range-minimum flag
+
+// the insertion steps of one chunk: block b inserts block-relative i = back(b) .. size - 12
+// (smallz4.h:612-625, 627); every block but the stream's first re-inserts the previous block's last
+// 12 positions, and the first of them (i = -12) was that block's last insertion: a duplicate whose
+// entries are both EndOfChain (its lastHash is itself, distance 0)
+struct DictPlan {
+  const Block* blocks;
+  uint32_t nb;
+  uint32_t cont;      // the first block continues the previous chunk's stream
+  uint32_t dictBack;  // first chunk: insertions start this far before block 0
+  uint32_t low0;      // reference dataZero at the first block (cont only)
+
+  __device__ __forceinline__ int64_t back(uint32_t b) const
+  {
+    return (b == 0 && !cont) ? -(int64_t)dictBack : -(int64_t)kTailNoMatch;
+  }
+  __device__ __forceinline__ bool dup_block(uint32_t b) const { return b != 0 || cont; }
+  // first position whose entries block b computes (the duplicate excluded)
+  __device__ __forceinline__ int64_t own_lo(uint32_t b) const
+  {
+    return (int64_t)blocks[b].start + (dup_block(b) ? -(int64_t)kTailNoMatch + 1 : back(b));
+  }
+  __device__ __forceinline__ int64_t own_hi(uint32_t b) const { return (int64_t)blocks[b].end - kTailNoMatch; }
+  // reference dataZero while block b is compressed (smallz4.h:799-804 keeps the last 64 KiB - 1)
+  __device__ __forceinline__ uint64_t low(uint32_t b) const
+  {
+    const int64_t l0 = cont ? (int64_t)low0 : 0;
+    if (b == 0) return (uint64_t)l0;
+    const int64_t l = (int64_t)blocks[b - 1].end - (int64_t)kWindow;
+    return (uint64_t)(l > l0 ? l : l0);
+  }
+};
+
+// the entry slot s holds at insertion step (b, it) of the chunk: written by the latest insertion at or
+// before it with block-relative index == s (mod 65536), or carried from the previous chunk.  `tab`
+// holds every non-duplicate insertion's entry at its staged position.
+__device__ __forceinline__ uint32_t read_slot(const DictPlan& P, const uint16_t* __restrict__ tab,
+                                              const uint16_t* __restrict__ carried, uint32_t s, uint32_t b, int64_t it,
+                                              uint64_t start, int64_t lo)
+{
+  int64_t iw = it - ((it - (int64_t)s) & (int64_t)kWindow);
+  if (iw >= lo) {  // in the current block (the common case)
+    if (iw == -(int64_t)kTailNoMatch && P.dup_block(b)) return 0u;
+    return tab[start + iw];
+  }
+  for (int32_t bb = (int32_t)b - 1; bb >= 0; bb--) {
+    const Block B = P.blocks[bb];
+    const int64_t hi = (int64_t)(B.end - B.start) - kTailNoMatch;
+    iw = hi - ((hi - (int64_t)s) & (int64_t)kWindow);
+    if (iw >= P.back((uint32_t)bb)) {
+      if (iw == -(int64_t)kTailNoMatch && P.dup_block((uint32_t)bb)) return 0u;
+      return tab[B.start + iw];
+    }
+  }
+  return carried[s];
+}
+
+__global__ __launch_bounds__(256) void k_dict_begin(uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
+                                                    uint16_t* __restrict__ prevX, uint32_t cont, uint32_t shift)
+{
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= (1u << kHashBits)) return;
+  if (!cont) {
+    last[j] = kDictNoPos;
+    if (j < 65536u) {
+      prevH[j] = 0;
+      prevX[j] = 0;
+    }
+  } else {
+    // chain slots are absolute positions mod 65536, unchanged by a shift that is a multiple of
+    // 65536; positions below the carried bytes become "no entry" (more than MaxDistance away)
+    const uint32_t v = last[j];
+    last[j] = (v == kDictNoPos || v < shift) ? kDictNoPos : v - shift;
+  }
+}
+
+// gate = 1 when a block holds an aligned 32 KiB window of one byte value (a run long enough for the
+// same-letter shortcut contains one)
+__global__ __launch_bounds__(256) void k_dict_detect(const uint8_t* __restrict__ in, uint64_t lo, uint64_t hi,
+                                                     uint32_t* __restrict__ gate)
+{
+  const uint64_t q = ((lo + 32767) & ~32767ull) + (uint64_t)blockIdx.x * 32768u;
+  if (q + 32768 > hi) return;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + q);
+  const uint32_t first = w[0] & 0xFFu;
+  const uint32_t all = first * 0x01010101u;
+  bool uniform = true;
+  for (uint32_t k = threadIdx.x; k < 8192u; k += 256u) uniform &= w[k] == all;
+  if (__syncthreads_and(uniform) && threadIdx.x == 0) atomicOr(gate, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_dict_keys(const uint8_t* __restrict__ in, uint64_t wlo, uint32_t n,
+                                                   uint64_t* __restrict__ keys)
+{
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= n) return;
+  keys[j] = ((uint64_t)ref_hash(gload4(in, wlo + j)) << kDictPosBits) | j;
+}
+
+__global__ __launch_bounds__(256) void k_dict_ph(const uint64_t* __restrict__ keys, uint32_t n, uint64_t wlo,
+                                                 uint64_t ownLo, const uint32_t* __restrict__ last,
+                                                 uint16_t* __restrict__ ph, const uint32_t* __restrict__ gate)
+{
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= n || *gate) return;
+  const uint64_t k = keys[j];
+  const uint64_t p = wlo + (k & kDictPosMask);
+  if (p < ownLo) return;  // below the block's own insertions: only a predecessor
+  const uint32_t h = (uint32_t)(k >> kDictPosBits);
+  uint64_t d = kNone;
+  if (j > 0 && (uint32_t)(keys[j - 1] >> kDictPosBits) == h) {
+    d = p - (wlo + (keys[j - 1] & kDictPosMask));
+  } else {
+    const uint32_t q = last[h];  // the previous chunk's (or an earlier block's) lastHash
+    if (q != kDictNoPos && q < p) d = p - q;
+  }
+  ph[p] = d <= kWindow ? (uint16_t)d : (uint16_t)0;
+}
+
+__global__ __launch_bounds__(256) void k_dict_last(const uint64_t* __restrict__ keys, uint32_t n, uint64_t wlo,
+                                                   uint64_t ownLo, uint32_t* __restrict__ last,
+                                                   const uint32_t* __restrict__ gate)
+{
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= n || *gate) return;
+  const uint64_t k = keys[j];
+  const uint64_t p = wlo + (k & kDictPosMask);
+  const uint32_t h = (uint32_t)(k >> kDictPosBits);
+  if (p >= ownLo && (j + 1 == n || (uint32_t)(keys[j + 1] >> kDictPosBits) != h)) last[h] = (uint32_t)p;
+}
+
+// previousExact (smallz4.h:668-720): from the previousHash candidate, follow the hash chain through
+// snapshot reads while the hash still matches; grid (positions, blocks)
+__global__ __launch_bounds__(256) void k_dict_pe(const uint8_t* __restrict__ in, DictPlan P,
+                                                 const uint16_t* __restrict__ ph, const uint16_t* __restrict__ prevH0,
+                                                 uint16_t* __restrict__ pe, const uint32_t* __restrict__ gate)
+{
+  if (*gate) return;
+  const uint32_t b = blockIdx.y;
+  const int64_t lo = P.own_lo(b), hi = P.own_hi(b);
+  const int64_t p = lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p > hi) return;
+  const uint64_t start = P.blocks[b].start;
+  const int64_t it = p - (int64_t)start, back = P.back(b);
+  const uint64_t low = P.low(b);
+  const uint32_t first = ph[p];
+  uint32_t exact = 0;
+  if (first) {
+    const uint32_t four = gload4(in, (uint64_t)p), h = ref_hash(four);
+    uint64_t cand = (uint64_t)p - first, dist = first;
+    bool ok = true;
+    while (true) {
+      if (cand < low) {  // the reference would read before its buffer
+        ok = false;
+        break;
+      }
+      const uint32_t seen = gload4(in, cand);
+      if (seen == four) break;
+      if (ref_hash(seen) != h) {
+        ok = false;
+        break;
+      }
+      const uint32_t step = read_slot(P, ph, prevH0, (uint32_t)(cand & kWindow), b, it, start, back);
+      if (!step) {
+        ok = false;
+        break;
+      }
+      dist += step;
+      if (dist > kWindow) {
+        ok = false;
+        break;
+      }
+      cand -= step;
+    }
+    exact = ok ? (uint32_t)dist : 0u;
+  }
+  pe[p] = (uint16_t)exact;
+}
+
+// findLongestMatch (smallz4.h:173-255) of every linked position (previousExact set) of every block,
+// over snapshot reads of the exact chains: strictly longer replaces, maxChain counts replacements.
+// Every other position gets (0, 0): not searched.  Grid (positions, blocks).
+__global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__ in, DictPlan P, uint32_t maxChain,
+                                                     const uint16_t* __restrict__ pe, const uint16_t* __restrict__ prevX0,
+                                                     uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag,
+                                                     const uint32_t* __restrict__ gate)
+{
+  if (*gate) return;
+  const uint32_t b = blockIdx.y;
+  const Block B = P.blocks[b];
+  const uint64_t size = B.end - B.start;
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= size) return;
+  const uint64_t pos = B.start + i;
+  if (maxChain > (uint32_t)kGreedyMax && i + kTailLiterals >= size) sel[pos] = 0;
+  uint32_t bestLen = 0, bestDist = 0;
+  if (i + kTailNoMatch <= size && pe[pos] != 0) {
+    const int64_t back = P.back(b);
+    const uint64_t stop = B.end - kTailLiterals;
+    bestLen = 1;
+    uint32_t steps = maxChain;
+    uint32_t hop = read_slot(P, pe, prevX0, (uint32_t)(pos & kWindow), b, (int64_t)i, B.start, back);
+    uint64_t backDist = 0;
+    const int64_t room = (int64_t)(stop - pos);
+    while (hop != 0) {
+      backDist += hop;
+      if (backDist > kWindow) break;
+      hop = read_slot(P, pe, prevX0, (uint32_t)((pos - backDist) & kWindow), b, (int64_t)i, B.start, back);
+      const int64_t need = (int64_t)bestLen + 1;
+      if (need > room) break;
+      const uint64_t c = pos - backDist;
+      // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
+      int64_t lo = need - 4;
+      while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
+      if (lo > 0) continue;
+      // phase 2: forward from the first new byte
+      int64_t hi = need;
+      while (hi + 4 <= room && gload4(in, pos + hi) == gload4(in, c + hi)) hi += 4;
+      while (hi < room && in[pos + hi] == in[c + hi]) hi++;
+      bestLen = (uint32_t)hi;
+      bestDist = (uint32_t)backDist;
+      if (--steps == 0) break;
+    }
+  }
+  mlen[pos] = bestLen;
+  mdist[pos] = (uint16_t)bestDist;
+  // optimal levels search every linked position: the parse's range-minimum flag is set here
+  if (maxChain > (uint32_t)kLazyMax) {
+    const bool rmq = bestLen >= kDictRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
+    if (__ballot(rmq) && lane_id() == 0) atomicOr(longFlag + b, 1u);
+  }
+}
+
+// Greedy/lazy levels: the skip bookkeeping (smallz4.h:726-744) over the linked positions of a block,
+// one wavefront per block.  A linked position is searched when skip is 0 or lazy evaluation is due;
+// the others are cleared.  Tiles of 16 windows of 64 positions; the next tile's loads are issued before
+// the current one is walked.
+constexpr int kSkipWin = 16;
+
+__global__ __launch_bounds__(64) void k_dict_skip(const Block* __restrict__ blocks, const uint16_t* __restrict__ pe,
+                                                  uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
+                                                  uint32_t* __restrict__ longFlag, const uint32_t* __restrict__ gate)
+{
+  if (*gate) return;
+  const Block B = blocks[blockIdx.x];
+  if (B.end - B.start < (uint64_t)kTailNoMatch) return;
+  const uint64_t start = B.start, last = B.end - kTailNoMatch;  // i + 12 <= size
+  const uint32_t lane = lane_id();
+  uint32_t skip = 0;
+  bool lazy = false, rmq = false;
+  uint32_t curL[kSkipWin], curE[kSkipWin], nxtL[kSkipWin], nxtE[kSkipWin];
+  auto load = [&](uint64_t tb, uint32_t* L, uint32_t* E) {
+#pragma unroll
+    for (int k = 0; k < kSkipWin; k++) {
+      const uint64_t p = tb + 64u * k + lane;
+      const uint64_t q = p <= last ? p : last;  // unconditional (clamped) loads, masked where used
+      L[k] = mlen[q];
+      E[k] = pe[q];
+    }
+  };
+  const uint64_t tile = 64u * kSkipWin;
+  uint64_t tb = start & ~63ull;
+  load(tb, curL, curE);
+  for (; tb <= last; tb += tile) {
+    load(tb + tile, nxtL, nxtE);
+#pragma unroll
+    for (int k = 0; k < kSkipWin; k++) {
+      const uint64_t p = tb + 64u * k + lane;
+      const bool linked = p >= start && p <= last && curE[k] != 0;
+      uint64_t m = __ballot(linked), kept = 0;
+      // no `continue` in this loop: hipcc (ROCm 7.2) dropped an assignment after one in a nested
+      // wave-uniform branch of the same shape
+      while (m) {
+        if (skip > 0 && !lazy) {
+          // the next `skip` linked positions are not searched
+          const uint32_t c = (uint32_t)__popcll(m);
+          if (skip >= c) {
+            skip -= c;
+            m = 0;
+          } else {
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            const uint64_t hit = __ballot(((m >> lane) & 1ull) && below == skip);
+            m &= ~0ull << __builtin_ctzll(hit);
+            skip = 0;
+          }
+        } else {
+          const uint32_t q = (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          if (skip > 0) {  // lazy evaluation: one more search (smallz4.h:728-733)
+            skip--;
+            lazy = false;
+          }
+          kept |= 1ull << q;
+          const uint32_t lq = rdlane(curL[k], q);
+          if (lq != 1u) {
+            lazy = skip == 0;
+            skip = lq;
+          }
+        }
+      }
+      const bool keep = (kept >> lane) & 1ull;
+      if (linked && !keep) {
+        mlen[p] = 0;
+        mdist[p] = 0;
+      }
+      // the distance is loaded only for the rare long match (a load here would be waited for in
+      // every window)
+      if (keep && curL[k] >= kDictRmqLen) rmq |= !(mdist[p] == 1u && curL[k] >= kSameLetter);
+    }
+#pragma unroll
+    for (int k = 0; k < kSkipWin; k++) {
+      curL[k] = nxtL[k];
+      curE[k] = nxtE[k];
+    }
+  }
+  if (__ballot(rmq) && lane == 0) longFlag[blockIdx.x] = 1u;
+}
+
+// the chain tables after the chunk's last insertion, in place (slot s reads only its own carried value)
+__global__ __launch_bounds__(256) void k_dict_carry(DictPlan P, const uint16_t* __restrict__ ph,
+                                                    const uint16_t* __restrict__ pe, uint16_t* __restrict__ prevH,
+                                                    uint16_t* __restrict__ prevX, const uint32_t* __restrict__ gate)
+{
+  if (*gate) return;
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= 65536u) return;
+  const uint32_t b = P.nb - 1;
+  const Block B = P.blocks[b];
+  const int64_t it = (int64_t)(B.end - B.start) - kTailNoMatch, back = P.back(b);
+  if (it < back) return;  // no insertion in the chunk (not reached: every block inserts)
+  const uint16_t h = (uint16_t)read_slot(P, ph, prevH, s, b, it, B.start, back);
+  const uint16_t x = (uint16_t)read_slot(P, pe, prevX, s, b, it, B.start, back);
+  prevH[s] = h;
+  prevX[s] = x;
+}
+
+uint64_t dict_sort_keys_max() { return kBlockMaxDict + kWindow + 64; }
+
+uint64_t dict_sort_temp_bytes()
+{
+  size_t bytes = 0;
+  rocprim::radix_sort_keys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)dict_sort_keys_max(), 0,
+                           kHashBits + kDictPosBits, (hipStream_t)0);
+  return bytes;
+}
+
+int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* hBlocks, uint32_t nb, uint32_t maxChain,
+                         uint32_t dictBack, uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH,
+                         uint16_t* prevX, uint16_t* ph, uint16_t* pe, uint64_t* keysA, uint64_t* keysB, void* temp,
+                         uint64_t tempBytes, uint32_t* gate, uint32_t* mlen, uint16_t* mdist, uint32_t* sel,
+                         uint32_t* longFlag, hipStream_t s)
+{
+  if (!nb) return 0;
+  if (hipMemsetAsync(gate, 0, 4, s)) return -1;
+  hipLaunchKernelGGL(k_dict_begin, dim3((1u << kHashBits) / 256), dim3(256), 0, s, last, prevH, prevX, cont, shift);
+  const uint64_t lo = hBlocks[0].start, hi = hBlocks[nb - 1].end;
+  const uint64_t wins = (hi - lo) / 32768 + 1;
+  hipLaunchKernelGGL(k_dict_detect, dim3((uint32_t)wins), dim3(256), 0, s, in, lo, hi, gate);
+  // the serial replay runs only for a gated chunk (its tables were prepared by k_dict_begin)
+  launch_dict_gated(in, dBlocks, nb, maxChain, dictBack, cont, shift, low0, last, prevH, prevX, mlen, mdist, sel, longFlag,
+                    gate, s);
+  DictPlan P{dBlocks, nb, cont, dictBack, low0};
+  // previousHash: per block, a sort of its own insertions and the 64 KiB below them
+  int64_t p0 = 0;
+  uint32_t maxOwn = 0, maxSize = 0;
+  for (uint32_t b = 0; b < nb; b++) {
+    const Block& B = hBlocks[b];
+    const bool dupB = b != 0 || cont;
+    const int64_t back = (b == 0 && !cont) ? -(int64_t)dictBack : -(int64_t)kTailNoMatch;
+    const int64_t ownLo = (int64_t)B.start + (dupB ? -(int64_t)kTailNoMatch + 1 : back);
+    const int64_t ownHi = (int64_t)B.end - kTailNoMatch;
+    if (b == 0) p0 = ownLo;
+    maxSize = std::max<uint32_t>(maxSize, (uint32_t)(B.end - B.start));
+    if (ownHi < ownLo) continue;
+    maxOwn = std::max<uint32_t>(maxOwn, (uint32_t)(ownHi - ownLo + 1));
+    const int64_t wlo = std::max<int64_t>(p0, ownLo - (int64_t)kWindow);
+    const uint32_t n = (uint32_t)(ownHi - wlo + 1);
+    if ((uint64_t)n > dict_sort_keys_max()) return -1;
+    const uint32_t g = (n + 255) / 256;
+    hipLaunchKernelGGL(k_dict_keys, dim3(g), dim3(256), 0, s, in, (uint64_t)wlo, n, keysA);
+    size_t tb = tempBytes;
+    if (rocprim::radix_sort_keys(temp, tb, keysA, keysB, (size_t)n, 0, kHashBits + kDictPosBits, s)) return -1;
+    hipLaunchKernelGGL(k_dict_ph, dim3(g), dim3(256), 0, s, keysB, n, (uint64_t)wlo, (uint64_t)ownLo, last, ph, gate);
+    hipLaunchKernelGGL(k_dict_last, dim3(g), dim3(256), 0, s, keysB, n, (uint64_t)wlo, (uint64_t)ownLo, last, gate);
+  }
+  if (maxOwn)
+    hipLaunchKernelGGL(k_dict_pe, dim3((maxOwn + 255) / 256, nb), dim3(256), 0, s, in, P, ph, prevH, pe, gate);
+  hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 255) / 256, nb), dim3(256), 0, s, in, P, maxChain, pe, prevX, mlen, mdist,
+                     sel, longFlag, gate);
+  if (maxChain <= (uint32_t)kLazyMax)
+    hipLaunchKernelGGL(k_dict_skip, dim3(nb), dim3(64), 0, s, dBlocks, pe, mlen, mdist, longFlag, gate);
+  hipLaunchKernelGGL(k_dict_carry, dim3(65536 / 256), dim3(256), 0, s, P, ph, pe, prevH, prevX, gate);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace sz4

@@ -131,6 +131,7 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
+  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictGate;  // dictionary mode on the whole GPU (sz4_dict.hip)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
@@ -149,6 +150,7 @@ struct sz4_ctx {
   std::vector<UnBlock> hUn;
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
+  bool dictSerial = getenv("SZ4_DICT_SERIAL") != nullptr;  // A/B and tests: the in-order replay for every chunk
 
   std::vector<Block> hBlocks;
   std::vector<Segment> hSegs;
@@ -177,7 +179,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictGate,
             &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
             &unOut, &unSeq};
   }
@@ -357,9 +359,26 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
     if ((e = c->dictLast.reserve(sizeof(uint32_t) << 20)) || (e = c->dictPrevH.reserve(2 * 65536)) ||
         (e = c->dictPrevX.reserve(2 * 65536)))
       return c->fail(SZ4_E_NOMEM, "dictionary tables", e);
-    launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
-                c->dictPrevH.as<uint16_t>(), c->dictPrevX.as<uint16_t>(), c->dictCont, c->dictShift, c->dictLow0,
-                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s);
+    if (c->dictLegacy || c->dictSerial) {
+      // legacy frames reset the tables every block: the reference's loop replayed in order
+      launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
+                  c->dictPrevH.as<uint16_t>(), c->dictPrevX.as<uint16_t>(), c->dictCont, c->dictShift, c->dictLow0,
+                  c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s);
+    } else {
+      const uint64_t staged = c->hBlocks.back().end + 64;
+      static const uint64_t tempBytes = dict_sort_temp_bytes();
+      if ((e = c->dictPH.reserve(staged * 2)) || (e = c->dictPE.reserve(staged * 2)) ||
+          (e = c->dictKeys.reserve(2 * dict_sort_keys_max() * 8)) || (e = c->dictTemp.reserve(tempBytes + 64)) ||
+          (e = c->dictGate.reserve(64)))
+        return c->fail(SZ4_E_NOMEM, "dictionary scratch", e);
+      if (launch_dict_parallel(in, dB, c->hBlocks.data(), nb, maxChain, (uint32_t)c->dictBack, c->dictCont, c->dictShift,
+                               c->dictLow0, c->dictLast.as<uint32_t>(), c->dictPrevH.as<uint16_t>(),
+                               c->dictPrevX.as<uint16_t>(), c->dictPH.as<uint16_t>(), c->dictPE.as<uint16_t>(),
+                               c->dictKeys.as<uint64_t>(), c->dictKeys.as<uint64_t>() + dict_sort_keys_max(), c->dictTemp.p,
+                               tempBytes, c->dictGate.as<uint32_t>(), c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(),
+                               c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s))
+        return c->fail(SZ4_E_DEVICE, "dictionary kernels");
+    }
     mark(c, 2, s);
     mark(c, 3, s);
     mark(c, 4, s);

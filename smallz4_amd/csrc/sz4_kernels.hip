@@ -25,6 +25,7 @@
 #include <type_traits>
 
 #include "sz4_internal.h"
+#include "sz4_device.h"
 
 #ifndef SZ4_SPEC_ATTR
 #define SZ4_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))  // 8 waves/SIMD (SGPR spills to lanes are cheap)
@@ -62,18 +63,6 @@ namespace sz4 {
 // ------------------------------------------------------------------------------------------------
 // small helpers
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t ref_hash(uint32_t four)
-{
-  return ((four * kHashMul) >> (32 - kHashBits)) & ((1u << kHashBits) - 1);
-}
-
-// four bytes at any offset of a buffer whose allocation is padded by >= 8 bytes and 4-aligned
-__device__ __forceinline__ uint32_t gload4(const uint8_t* base, uint64_t off)
-{
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
-  const uint32_t lo = w[0], hi = w[1];
-  return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
-}
 
 __device__ __forceinline__ uint32_t lload4(const uint32_t* w, uint32_t off)
 {
@@ -81,7 +70,6 @@ __device__ __forceinline__ uint32_t lload4(const uint32_t* w, uint32_t off)
   return __builtin_amdgcn_alignbyte(hi, lo, off & 3);
 }
 
-__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 {
@@ -133,11 +121,6 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
   return v;
 }
 
-// value of a lane chosen by a wave-uniform index (v_readlane: no LDS round trip)
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, uint32_t lane)
-{
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
-}
 
 // DPP row (16-lane) permutations
 #if SZ4_DIAG >= 3
@@ -762,16 +745,21 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 // preceding byte -- records, markup, tables -- so that they carry from p-1 and k_find_big's
 // left-maximal search only visits the few others.  Decided on kLpfProbe candidates spread over the
 // group below the target: at least kLpfProbe - 2 of them share its preceding byte `cls`.
+#ifndef SZ4_LPF_LONG
+#define SZ4_LPF_LONG 0
+#endif
+constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
 template <class Src>
 __device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint32_t gs, uint32_t slot, uint32_t cls,
-                                           uint64_t w0, uint64_t predLo, const Src& src)
+                                           uint64_t w0, uint64_t predLo, uint32_t me1, uint32_t me2, const Src& src)
 {
-  uint32_t same = 0;
+  uint32_t same = 0, longer = 0;
   for (uint32_t k = 0; k < kLpfProbe; k++) {
     const uint64_t q = w0 + slot_pos(compact, small, gs + (uint32_t)((uint64_t)(slot - gs) * k / kLpfProbe));
     same += q > predLo && (src.ld4(q - 1) & 0xFFu) == cls ? 1u : 0u;
+    if constexpr (kLpfLong > 0) longer += src.ld4(q + 4) == me1 && src.ld4(q + 8) == me2 ? 1u : 0u;
   }
-  return same + 2u >= kLpfProbe;
+  return same + 2u >= kLpfProbe && longer >= kLpfLong;
 }
 
 template <bool kLds>
@@ -909,7 +897,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
                      (slot - gs > kBigGroup ||
                       (lpfOk && ((run_key(me0) && slot - gs > (lpfBlock ? kBigRunL : kBigRun)) ||
                                  (lpfBlock && slot - gs > kLpfMin && p > predLoF &&
-                                  lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, src)))));
+                                  lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, me1, me2, src)))));
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
@@ -3459,9 +3447,13 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
                                                      uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
                                                      uint16_t* __restrict__ prevXg, uint32_t cont, uint32_t shift,
                                                      uint32_t low0, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
+                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag,
+                                                     const uint32_t* __restrict__ gate)
 {
   __shared__ uint16_t prevX[65536];
+  // gate: the data-parallel path (sz4_dict.hip) takes the chunk unless k_dict_detect set it, and its
+  // k_dict_begin has already prepared the carried tables
+  if (gate && *gate == 0u) return;
   const uint32_t lane = threadIdx.x;
   auto reset = [&]() {
     for (uint32_t j = lane; j < 65536; j += 64) {
@@ -3470,7 +3462,9 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
     }
     for (uint32_t j = lane; j < (1u << kHashBits); j += 64) last[j] = kNoPos;
   };
-  if (!cont) {
+  if (gate) {
+    for (uint32_t j = lane; j < 65536; j += 64) prevX[j] = prevXg[j];
+  } else if (!cont) {
     reset();
   } else {
     // the previous chunk's tables: chain slots are absolute positions mod 65536, unchanged by a shift
@@ -3603,7 +3597,17 @@ void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint3
 {
   if (nblocks)
     hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, legacy, last, prevH,
-                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag);
+                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag, (const uint32_t*)nullptr);
+}
+
+void launch_dict_gated(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack,
+                       uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH, uint16_t* prevX,
+                       uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, const uint32_t* gate,
+                       hipStream_t s)
+{
+  if (nblocks)
+    hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, 0, last, prevH,
+                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag, gate);
 }
 
 // Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut

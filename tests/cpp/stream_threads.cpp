@@ -6,7 +6,9 @@
 //   stream_threads big <level> <base> <reps> <out>
 //       one long stream through smallz4::lz4: <base> repeated <reps> times, repetition r with the
 //       8 bytes at offset (r * 7919) % size replaced by r (little endian); prints the library's
-//       device footprint (sz4_device_bytes of the pooled context) and the stream's length
+//       device footprint (sz4_device_bytes of the pooled context), the stream's length and its
+//       wall-clock rate (the whole smallz4::lz4 call: callbacks, PCIe both ways, kernels)
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -123,13 +125,16 @@ int main(int argc, char** argv)
     std::vector<unsigned char> base = read_file(argv[3]);
     Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, fopen(argv[5], "wb"), 0};
     b.total = b.reps * base.size();
+    const auto t0 = std::chrono::steady_clock::now();
     smallz4::lz4(get_big, send_big, chain, false, &b);
+    const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     fclose(b.out);
     // the footprint of the pooled context the call used (handed back to the pool, borrowed again)
     sz4_ctx* c = NULL;
     sz4_acquire(&c, getenv("SMALLZ4_AMD_DEVICE") ? atoi(getenv("SMALLZ4_AMD_DEVICE")) : 0);
-    printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu}\n", (unsigned long long)b.total,
-           (unsigned long long)b.sent, (unsigned long long)sz4_device_bytes(c));
+    printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu, \"seconds\": %.3f, \"MB/s\": %.1f}\n",
+           (unsigned long long)b.total, (unsigned long long)b.sent, (unsigned long long)sz4_device_bytes(c), secs,
+           b.total / secs / 1e6);
     sz4_release(c);
     return 0;
   }

@@ -231,12 +231,18 @@ def test_stream_run_across_block_boundary(compressor):
 @pytest.mark.parametrize("chain", [3, 6, 9, 65535])
 def test_dictionary_mode(compressor, chain):
     """Dictionary mode reproduces the reference byte for byte, including its misaligned chain slots
-    (DESIGN.md section 3.7): k_dict_matches replays the match loop, the parse and assembly are shared."""
+    (DESIGN.md section 3.7): the data-parallel snapshot reads of sz4_dict.hip for modern frames, the
+    in-order replay (k_dict_matches) for legacy ones; the parse and assembly are shared."""
     cases = [
         (synth.enwik8_like(60000, seed=50), synth.enwik8_like(20000, seed=51), False),
         (synth.enwik8_like(40000, seed=52), synth.enwik8_like(70000, seed=53), False),
         (bytes(20) + synth.enwik8_like(30000, seed=54), b"short dictionary", False),
         (synth.enwik8_like(30000, seed=55), synth.enwik8_like(5000, seed=56), True),
+        # runs and periodic data: long phase-2 extensions, hash-collision walks, duplicate re-insertions
+        (bytes(20000) + synth.enwik8_like(20000, seed=57) * 3, b"\0" * 500 + b"xyz" * 3000, False),
+        (b"abcd" * 5000 + synth.random_bytes(50000, seed=58), synth.random_bytes(70000, seed=59), False),
+        (b"", synth.enwik8_like(1000, seed=60), False),
+        (b"tiny", synth.enwik8_like(1000, seed=61), False),
     ]
     for data, dictionary, legacy in cases:
         assert compressor.lz4(data, chain, dictionary, legacy) == pyoracle.oz_lz4(data, chain, dictionary, legacy)

@@ -83,16 +83,39 @@ def test_decoder_stream_rejects_huge_block_word(compressor):
         _decode_stream(compressor, frame)
 
 
-@pytest.mark.parametrize("legacy", [False, True])
-@pytest.mark.parametrize("chain", [3, 6])
+@pytest.mark.parametrize("legacy,chain", [(False, 3), (False, 6), (False, 65535), (True, 3), (True, 6)])
 def test_chunked_dictionary(chunked, chain, legacy):
     """Dictionary mode carries the reference's hash table and both chains across chunks (their slots
-    are absolute positions mod 65536: chunks move by multiples of 65536).  Dictionary mode replays the
-    reference's loop in one wavefront, so the multi-chunk case runs at short
-    chains; -9 with a dictionary is covered on one chunk (test_gpu.py::test_dictionary_mode)."""
+    are absolute positions mod 65536: chunks move by multiples of 65536).  Modern frames take the
+    data-parallel path (sz4_dict.hip), legacy frames replay the reference's loop in one wavefront
+    (DESIGN.md section 3.7), so those run at short chains only."""
     data = synth.enwik8_like(2 * M + 300000, seed=66)
     dictionary = synth.enwik8_like(50000, seed=67)
     assert chunked.lz4(data, chain, dictionary, legacy) == pyoracle.oz_lz4(data, chain, dictionary, legacy)
+
+
+@pytest.mark.parametrize("chain", [3, 65535])
+def test_chunked_dictionary_multi_block_chunks(compressor, chain):
+    """Chunks of two 4 MiB blocks with a dictionary: the snapshot reads of the chain slots cross a block
+    boundary inside a chunk and the carried tables cross the chunk boundary."""
+    data = synth.enwik8_like(4 * M + 123457, seed=68)
+    dictionary = synth.enwik8_like(65536, seed=69)
+    compressor.set_stream_chunk(2 * M)
+    try:
+        assert compressor.lz4(data, chain, dictionary) == pyoracle.oz_lz4(data, chain, dictionary)
+    finally:
+        compressor.set_stream_chunk(0)
+
+
+@pytest.mark.parametrize("chain", [3, 6])
+def test_dictionary_long_run_gate(chunked, chain):
+    """A run of one byte value long enough for the same-letter shortcut (> 65 300 bytes) sends its chunk
+    to the in-order replay (k_dict_detect's gate); the next chunk continues on the data-parallel path
+    from the tables the replay left.  Short runs (< 32 KiB windows) stay on the parallel path."""
+    data = (synth.enwik8_like(M - 120000, seed=70) + b"a" * 70000 + synth.enwik8_like(50000, seed=71) +
+            bytes(30000) + synth.enwik8_like(M // 2, seed=72))
+    dictionary = b"a" * 1000 + synth.enwik8_like(9000, seed=73)
+    assert chunked.lz4(data, chain, dictionary) == pyoracle.oz_lz4(data, chain, dictionary)
 
 
 @pytest.mark.parametrize("chain", [3, 65535])
