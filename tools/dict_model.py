@@ -1,0 +1,165 @@
+#!/usr/bin/env python3
+"""Model check of the data-parallel dictionary mode (smallz4_amd/csrc/sz4_dict.hip)
+against the in-order replay (k_dict_matches), in pure Python at small block sizes (multiples of 65536 keep
+the dictionary's 65535 mod 65536 alignment): match arrays and final chain tables must be identical.
+Diagnostic, CPU only: python tools/dict_model.py (about a minute)."""
+import sys, random
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
+from smallz4_amd import synth
+W = 65535
+def h32(f): return ((f * 48271) & 0xFFFFFFFF) >> 12
+def ld4(d, p): return int.from_bytes(d[p:p+4].ljust(4, b'\0'), 'little')
+
+def serial(data, blocks, dictBack, maxChain):
+    last = {}; prevH = [0]*65536; prevX = [0]*65536
+    mlen = {}; mdist = {}; low = 0; withDict = True
+    for (start, end) in blocks:
+        size = end - start; stop = end - 5
+        back = -dictBack if withDict else -12
+        i = back
+        while i + 12 <= size:
+            pos = start + i
+            slot = i & W
+            four = ld4(data, pos); h = h32(four)
+            cand = last.get(h); last[h] = pos
+            linked = False
+            if cand is None or pos - cand > W:
+                prevH[slot] = 0; prevX[slot] = 0
+            else:
+                dist = pos - cand; prevH[slot] = dist; ok = True
+                while True:
+                    if cand < low: ok = False; break
+                    seen = ld4(data, cand)
+                    if seen == four: break
+                    if h32(seen) != h: ok = False; break
+                    step = prevH[cand & W]
+                    if step == 0: ok = False; break
+                    dist += step
+                    if dist > W: ok = False; break
+                    cand -= step
+                    if cand < low: ok = False; break
+                prevX[slot] = dist if ok else 0
+                linked = ok and dist != 0
+            if linked and i >= 0:
+                bestLen, bestDist, steps = 1, 0, maxChain
+                hop = prevX[pos & W]; bd = 0; room = stop - pos
+                while hop:
+                    bd += hop
+                    if bd > W: break
+                    hop = prevX[(pos - bd) & W]
+                    need = bestLen + 1
+                    if need > room: break
+                    c = pos - bd
+                    lo = need - 4
+                    while lo > 0 and ld4(data, pos+lo) == ld4(data, c+lo): lo -= 4
+                    if lo > 0: continue
+                    hi = need
+                    while hi + 4 <= room and ld4(data, pos+hi) == ld4(data, c+hi): hi += 4
+                    while hi < room and data[pos+hi] == data[c+hi]: hi += 1
+                    bestLen, bestDist = hi, bd
+                    steps -= 1
+                    if steps == 0: break
+                mlen[pos] = bestLen; mdist[pos] = bestDist
+            i += 1
+        withDict = False
+        if end - low > W: low = end - W
+    return mlen, mdist, prevH, prevX
+
+def parallel(data, blocks, dictBack, maxChain):
+    nb = len(blocks); cont = 0
+    def back(b): return -dictBack if (b == 0 and not cont) else -12
+    def dup(b): return b != 0 or cont
+    def own_lo(b): return blocks[b][0] + (-11 if dup(b) else back(b))
+    def own_hi(b): return blocks[b][1] - 12
+    def lowb(b): return 0 if b == 0 else max(0, blocks[b-1][1] - W)
+    ph = {}; pe = {}; last = {}
+    p0 = own_lo(0)
+    for b in range(nb):
+        lo, hi = own_lo(b), own_hi(b)
+        if hi < lo: continue
+        wlo = max(p0, lo - W)
+        keys = sorted((h32(ld4(data, p)), p) for p in range(wlo, hi + 1))
+        for j, (h, p) in enumerate(keys):
+            if p < lo: continue
+            d = None
+            if j > 0 and keys[j-1][0] == h: d = p - keys[j-1][1]
+            else:
+                q = last.get(h)
+                if q is not None and q < p: d = p - q
+            ph[p] = d if d is not None and d <= W else 0
+        for j, (h, p) in enumerate(keys):
+            if p >= lo and (j + 1 == len(keys) or keys[j+1][0] != h): last[h] = p
+    def read_slot(tab, s, b, it):
+        start = blocks[b][0]
+        iw = it - ((it - s) & W)
+        if iw >= back(b):
+            if iw == -12 and dup(b): return 0
+            return tab[start + iw]
+        for bb in range(b - 1, -1, -1):
+            st, en = blocks[bb]; hi = en - st - 12
+            iw = hi - ((hi - s) & W)
+            if iw >= back(bb):
+                if iw == -12 and dup(bb): return 0
+                return tab[st + iw]
+        return 0
+    for b in range(nb):
+        start = blocks[b][0]; low = lowb(b)
+        for p in range(own_lo(b), own_hi(b) + 1):
+            it = p - start; first = ph[p]; exact = 0
+            if first:
+                four = ld4(data, p); h = h32(four); cand = p - first; dist = first; ok = True
+                while True:
+                    if cand < low: ok = False; break
+                    seen = ld4(data, cand)
+                    if seen == four: break
+                    if h32(seen) != h: ok = False; break
+                    step = read_slot(ph, cand & W, b, it)
+                    if not step: ok = False; break
+                    dist += step
+                    if dist > W: ok = False; break
+                    cand -= step
+                exact = dist if ok else 0
+            pe[p] = exact
+    mlen = {}; mdist = {}
+    for b in range(nb):
+        start, end = blocks[b]; size = end - start; stop = end - 5
+        for i in range(0, size - 12 + 1):
+            pos = start + i
+            if pe[pos] == 0: continue
+            bestLen, bestDist, steps = 1, 0, maxChain
+            hop = read_slot(pe, pos & W, b, i); bd = 0; room = stop - pos
+            while hop:
+                bd += hop
+                if bd > W: break
+                hop = read_slot(pe, (pos - bd) & W, b, i)
+                need = bestLen + 1
+                if need > room: break
+                c = pos - bd
+                lo = need - 4
+                while lo > 0 and ld4(data, pos+lo) == ld4(data, c+lo): lo -= 4
+                if lo > 0: continue
+                hi = need
+                while hi + 4 <= room and ld4(data, pos+hi) == ld4(data, c+hi): hi += 4
+                while hi < room and data[pos+hi] == data[c+hi]: hi += 1
+                bestLen, bestDist = hi, bd
+                steps -= 1
+                if steps == 0: break
+            mlen[pos] = bestLen; mdist[pos] = bestDist
+    b = nb - 1; it = blocks[b][1] - blocks[b][0] - 12
+    cH = [read_slot(ph, s, b, it) for s in range(65536)]
+    cX = [read_slot(pe, s, b, it) for s in range(65536)]
+    return mlen, mdist, cH, cX
+
+for (bs, n, dl, chain, seed) in [(131072, 300000, 20000, 65535, 1), (65536*2, 280000, 65535, 5, 2), (65536*3, 200000, 3000, 65535, 3)]:
+    dic = synth.enwik8_like(dl, seed=seed)
+    body = synth.enwik8_like(n, seed=seed+10)
+    dictBack = min(dl, W)
+    prefix = (b'\0' * W + dic)[-W:]
+    data = prefix + body + b'\0' * 16
+    blocks = []
+    s = W
+    while s < W + n:
+        blocks.append((s, min(s + bs, W + n))); s += bs
+    a = serial(data, blocks, dictBack, chain)
+    b = parallel(data, blocks, dictBack, chain)
+    print(bs, n, dl, chain, 'mlen', a[0] == b[0], 'mdist', a[1] == b[1], 'prevH', a[2] == b[2], 'prevX', a[3] == b[3], len(a[0]))
