@@ -54,6 +54,14 @@
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
+#ifndef SZ4_HBM_GLOBAL  // k_find_sorted_hbm reads the text from HBM/L2 (no LDS window): two workgroups per CU
+#define SZ4_HBM_GLOBAL 1
+#endif
+#if SZ4_HBM_GLOBAL
+#define SZ4_HBM_SGPR 80
+#else
+#define SZ4_HBM_SGPR 96
+#endif
 #ifndef SZ4_DIAG
 #define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
 #endif
@@ -826,9 +834,17 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     s_next = 0;
     s_long = 0;
   }
-  // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM
+  // kLds: the block's whole window in LDS; otherwise (SZ4_HBM_GLOBAL) every byte from HBM/L2, so that
+  // the LDS holds only the sort and the result tiles and two workgroups share a CU -- the candidates'
+  // first 12 bytes live in registers, so text reads are per chunk and per extension, not per
+  // candidate -- or [w0, s1 + 64) in LDS and the rest from HBM
+#if SZ4_HBM_GLOBAL
+  typename std::conditional<kLds, Bytes<true>, Bytes<false>>::type src;
+  if constexpr (kLds) {
+#else
   typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
   {
+#endif
     const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
     const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
     for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
@@ -839,6 +855,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       src.in = in;
     }
   }
+#if SZ4_HBM_GLOBAL
+  if constexpr (!kLds) src.in = in;
+#endif
   __syncthreads();
 
   uint64_t cut = B.cut;
@@ -1486,7 +1505,7 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(80)
 {
   find_sorted_body<true>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
 }
-__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(96))) void k_find_sorted_hbm(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(SZ4_HBM_SGPR))) void k_find_sorted_hbm(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                 const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                 const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
                                 uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
@@ -5369,7 +5388,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
   } else {
     if (pass == 1) {
       // the sort and the text-order result tiles use the same buffer: at least 64 KiB
-      const uint32_t lds = hybridLds > kOutTile * 4u ? hybridLds : kOutTile * 4u;
+      const uint32_t lds = (hybridLds > kOutTile * 4u && !SZ4_HBM_GLOBAL) ? hybridLds : kOutTile * 4u;
       hipFuncSetAttribute((const void*)k_find_sorted_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k_find_sorted_hbm, dim3(nsegs), dim3(kFindThreads), lds, s, in, segs, blocks, iv, ivCount,
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
