@@ -26,7 +26,8 @@
 //   k_dict_last     the hash table's final positions (lastHash, smallz4.h:650-652)
 //   k_dict_pe       previousExact of every insertion: the hash-chain walk over snapshot reads
 //   k_dict_search   findLongestMatch of every linked position of every block
-//   k_dict_skip     greedy/lazy levels: the reference's skip bookkeeping (smallz4.h:726-744), per block
+//   k_dict_lz_*     greedy/lazy levels: the reference's skip bookkeeping (smallz4.h:726-744), walked
+//                   speculatively per 4096-position sub-segment and repaired per block
 //   k_dict_carry    the final chain tables, for the next chunk
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -278,89 +279,231 @@ __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__
   }
 }
 
-// Greedy/lazy levels: the skip bookkeeping (smallz4.h:726-744) over the linked positions of a block,
-// one wavefront per block.  A linked position is searched when skip is 0 or lazy evaluation is due;
-// the others are cleared.  Tiles of 16 windows of 64 positions; the next tile's loads are issued before
-// the current one is walked.
-constexpr int kSkipWin = 16;
+// Greedy/lazy levels: the skip bookkeeping (smallz4.h:726-744) over the linked positions of a block
+// (previousExact set, i >= 0).  Between searches the reference's state is (next searched position,
+// mode, carry):
+//   fresh search at q (skip 0), length L:  L == 1 -> the next linked position is searched fresh;
+//                                          else   -> the next one is searched lazily, carry = L - 1;
+//   lazy search at q, length L2:           the next (L2 != 1 ? L2 : carry) linked positions are
+//                                          skipped, the one after is searched fresh.
+// (A search that finds nothing, length 1, is possible here: the snapshot chains need not lead to a
+// match.)  A fresh position fixes the whole future, so the chain is walked speculatively per
+// kWalkSeg sub-segment from its first linked position (k_dict_lz_walk: searched and fresh positions as
+// bit masks), k_dict_lz_fix walks a block's sub-segments in order and re-walks from the true entry until
+// it reaches a position the speculative walk searched fresh, and k_dict_lz_clear clears the linked
+// positions nobody searched.  Masks: kWalkSeg bits each, [fresh | kept] per sub-segment.
+constexpr uint32_t kLzWords = kWalkSeg / 32;
+constexpr uint32_t kLzEnd = 0x7FFFFFFFu;
 
-__global__ __launch_bounds__(64) void k_dict_skip(const Block* __restrict__ blocks, const uint16_t* __restrict__ pe,
-                                                  uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                  uint32_t* __restrict__ longFlag, const uint32_t* __restrict__ gate)
-{
-  if (*gate) return;
-  const Block B = blocks[blockIdx.x];
-  if (B.end - B.start < (uint64_t)kTailNoMatch) return;
-  const uint64_t start = B.start, last = B.end - kTailNoMatch;  // i + 12 <= size
-  const uint32_t lane = lane_id();
-  uint32_t skip = 0;
-  bool lazy = false, rmq = false;
-  uint32_t curL[kSkipWin], curE[kSkipWin], nxtL[kSkipWin], nxtE[kSkipWin];
-  auto load = [&](uint64_t tb, uint32_t* L, uint32_t* E) {
-#pragma unroll
-    for (int k = 0; k < kSkipWin; k++) {
-      const uint64_t p = tb + 64u * k + lane;
-      const uint64_t q = p <= last ? p : last;  // unconditional (clamped) loads, masked where used
-      L[k] = mlen[q];
-      E[k] = pe[q];
-    }
-  };
-  const uint64_t tile = 64u * kSkipWin;
-  uint64_t tb = start & ~63ull;
-  load(tb, curL, curE);
-  for (; tb <= last; tb += tile) {
-    load(tb + tile, nxtL, nxtE);
-#pragma unroll
-    for (int k = 0; k < kSkipWin; k++) {
-      const uint64_t p = tb + 64u * k + lane;
-      const bool linked = p >= start && p <= last && curE[k] != 0;
-      uint64_t m = __ballot(linked), kept = 0;
-      // no `continue` in this loop: hipcc (ROCm 7.2) dropped an assignment after one in a nested
-      // wave-uniform branch of the same shape
-      while (m) {
-        if (skip > 0 && !lazy) {
-          // the next `skip` linked positions are not searched
-          const uint32_t c = (uint32_t)__popcll(m);
-          if (skip >= c) {
-            skip -= c;
-            m = 0;
-          } else {
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            const uint64_t hit = __ballot(((m >> lane) & 1ull) && below == skip);
-            m &= ~0ull << __builtin_ctzll(hit);
-            skip = 0;
-          }
+// the need-th (0-based) linked position at or after pos over a register window of 64 positions
+// (loads three windows ahead, unconditional with a clamped index as in k_walk)
+struct DictWalker {
+  const uint32_t* L;
+  const uint16_t* E;
+  uint32_t last;  // inclusive
+  uint32_t wbase, wL, wE, xL1, xE1, xL2, xE2, xL3, xE3;
+  __device__ __forceinline__ void ld(uint32_t b, uint32_t& l, uint32_t& e) const
+  {
+    const uint32_t i = b + lane_id();
+    const uint32_t j = i <= last ? i : last;
+    l = L[j];
+    e = E[j];
+  }
+  __device__ __forceinline__ void start(uint32_t pos)
+  {
+    wbase = pos & ~63u;
+    ld(wbase, wL, wE);
+    ld(wbase + 64, xL1, xE1);
+    ld(wbase + 128, xL2, xE2);
+    ld(wbase + 192, xL3, xE3);
+  }
+  __device__ __forceinline__ uint32_t next(uint32_t pos, uint32_t need)
+  {
+    while (pos <= last) {
+      while (pos >= wbase + 64) {
+        if (pos < wbase + 256) {
+          wbase += 64;
+          wL = xL1;
+          wE = xE1;
+          xL1 = xL2;
+          xE1 = xE2;
+          xL2 = xL3;
+          xE2 = xE3;
+          ld(wbase + 192, xL3, xE3);
         } else {
-          const uint32_t q = (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          if (skip > 0) {  // lazy evaluation: one more search (smallz4.h:728-733)
-            skip--;
-            lazy = false;
-          }
-          kept |= 1ull << q;
-          const uint32_t lq = rdlane(curL[k], q);
-          if (lq != 1u) {
-            lazy = skip == 0;
-            skip = lq;
-          }
+          start(pos);
         }
       }
-      const bool keep = (kept >> lane) & 1ull;
-      if (linked && !keep) {
+      const uint64_t mask = __ballot(wE != 0u && wbase + lane_id() <= last) & (~0ull << (pos - wbase));
+      const uint32_t pc = (uint32_t)__popcll(mask);
+      if (need < pc) {
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+        const uint64_t hit = __ballot(((mask >> lane_id()) & 1ull) && below == need);
+        return wbase + (uint32_t)__builtin_ctzll(hit);
+      }
+      need -= pc;
+      pos = wbase + 64;
+    }
+    return kLzEnd;
+  }
+  __device__ __forceinline__ uint32_t len(uint32_t q) const { return rdlane(wL, q - wbase); }
+};
+
+// one step of the chain from the searched position q (mode md: 0 fresh, 1 lazy; carry: see above)
+__device__ __forceinline__ uint32_t lz_step(DictWalker& w, uint32_t q, uint32_t& md, uint32_t& carry)
+{
+  const uint32_t L = w.len(q);
+  if (md == 0u) {
+    if (L != 1u) {
+      carry = L - 1u;
+      md = 1u;
+    }
+    return w.next(q + 1, 0u);
+  }
+  md = 0u;
+  return w.next(q + 1, L != 1u ? L : carry);
+}
+
+__device__ __forceinline__ void lz_setbit(uint32_t* m, uint32_t i)
+{
+  if (lane_id() == 0) m[i >> 5] |= 1u << (i & 31);
+}
+
+__global__ __launch_bounds__(64 * 4) void k_dict_lz_walk(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
+                                                         uint32_t nwalk, const uint32_t* __restrict__ mlen,
+                                                         const uint16_t* __restrict__ pe, uint32_t* __restrict__ masks,
+                                                         uint4* __restrict__ state, const uint32_t* __restrict__ gate)
+{
+  __shared__ uint32_t bits[4][2 * kLzWords];
+  if (*gate) return;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * 4 + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  uint32_t* fresh = bits[wave];
+  uint32_t* kept = fresh + kLzWords;
+  for (uint32_t t = lane; t < 2 * kLzWords; t += 64) fresh[t] = 0;
+  const uint32_t a = ws.y * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+  DictWalker w;
+  w.L = mlen + B.start;
+  w.E = pe + B.start;
+  w.last = n - kTailNoMatch;
+  w.start(a);
+  uint32_t md = 0, carry = 0;
+  uint32_t q = w.next(a, 0u);  // assumed: the sub-segment's first linked position, searched fresh
+  __builtin_amdgcn_wave_barrier();
+  while (q < aNext) {
+    lz_setbit(kept, q - a);
+    if (md == 0u) lz_setbit(fresh, q - a);
+    q = lz_step(w, q, md, carry);
+  }
+  __builtin_amdgcn_wave_barrier();
+  uint32_t* out = masks + (uint64_t)idx * (2 * kLzWords);
+  for (uint32_t t = lane; t < 2 * kLzWords; t += 64) out[t] = fresh[t];
+  if (lane == 0) state[idx] = make_uint4(q, md, carry, 0u);
+}
+
+__global__ __launch_bounds__(64) void k_dict_lz_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ mlen,
+                                                    const uint16_t* __restrict__ pe, uint32_t* __restrict__ masks,
+                                                    uint4* __restrict__ state, const uint32_t* __restrict__ gate)
+{
+  __shared__ uint32_t fresh[kLzWords], rep[kLzWords];
+  if (*gate) return;
+  const Block B = blocks[blockIdx.x];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch || B.walkCount < 2) return;
+  DictWalker w;
+  w.L = mlen + B.start;
+  w.E = pe + B.start;
+  w.last = n - kTailNoMatch;
+  w.wbase = 0xFFFFFFC0u;  // no window loaded yet
+  uint4 ex = state[B.walkFirst];  // sub-segment 0 was walked from the block start: exact
+  for (uint32_t k = 1; k < B.walkCount; k++) {
+    const uint32_t idx = B.walkFirst + k;
+    const uint4 spec = state[idx];
+    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+    uint32_t* m = masks + (uint64_t)idx * (2 * kLzWords);
+    uint32_t q = ex.x, md = ex.y, carry = ex.z;
+    if (q >= aNext) {  // nothing searched in this sub-segment
+      for (uint32_t t = lane; t < kLzWords; t += 64) m[kLzWords + t] = 0;
+      continue;  // ex unchanged: the entry of the next sub-segment
+    }
+    for (uint32_t t = lane; t < kLzWords; t += 64) {
+      fresh[t] = m[t];
+      rep[t] = 0;
+    }
+    __syncthreads();
+    auto is_fresh = [&](uint32_t p) { return (fresh[(p - a) >> 5] >> ((p - a) & 31)) & 1u; };
+    // the speculative walk is right from its first fresh position at or after the true entry on;
+    // before it, re-walk from the true entry
+    bool merged = md == 0u && is_fresh(q);
+    if (!merged) {
+      if (w.wbase == 0xFFFFFFC0u || q < w.wbase || q >= w.wbase + 256) w.start(q);
+      (void)w.next(q, 0u);  // q is linked: brings its window in
+      while (q < aNext) {
+        if (md == 0u && is_fresh(q)) {
+          merged = true;
+          break;
+        }
+        lz_setbit(rep, q - a);
+        q = lz_step(w, q, md, carry);
+      }
+    }
+    __syncthreads();
+    // kept = the re-walked positions, then the speculative ones from the merge point on
+    const uint32_t from = merged ? q - a : kWalkSeg;
+    for (uint32_t t = lane; t < kLzWords; t += 64) {
+      const uint32_t lo = t * 32;
+      const uint32_t keepSpec = from <= lo ? 0xFFFFFFFFu : (from >= lo + 32 ? 0u : ~0u << (from - lo));
+      m[kLzWords + t] = rep[t] | (m[kLzWords + t] & keepSpec);
+    }
+    ex = merged ? spec : make_uint4(q, md, carry, 0u);
+    __syncthreads();
+  }
+}
+
+// linked positions no walk searched get (0, 0); the parse's range-minimum flag over the searched ones
+__global__ __launch_bounds__(64 * 4) void k_dict_lz_clear(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
+                                                          uint32_t nwalk, uint32_t* __restrict__ mlen,
+                                                          uint16_t* __restrict__ mdist, const uint16_t* __restrict__ pe,
+                                                          const uint32_t* __restrict__ masks, uint32_t* __restrict__ longFlag,
+                                                          const uint32_t* __restrict__ gate)
+{
+  if (*gate) return;
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * 4 + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t last = n - kTailNoMatch;
+  const uint32_t a = ws.y * kWalkSeg;
+  const uint32_t hi = a + kWalkSeg - 1 < last ? a + kWalkSeg - 1 : last;  // inclusive
+  const uint32_t* kept = masks + (uint64_t)idx * (2 * kLzWords) + kLzWords;
+  bool rmq = false;
+  for (uint32_t x0 = a; x0 <= hi; x0 += 64) {
+    const uint32_t x = x0 + lane;
+    if (x > hi) break;
+    const uint64_t p = B.start + x;
+    const bool keep = (kept[(x - a) >> 5] >> ((x - a) & 31)) & 1u;
+    if (!keep) {
+      if (pe[p] != 0u) {
         mlen[p] = 0;
         mdist[p] = 0;
       }
-      // the distance is loaded only for the rare long match (a load here would be waited for in
-      // every window)
-      if (keep && curL[k] >= kDictRmqLen) rmq |= !(mdist[p] == 1u && curL[k] >= kSameLetter);
-    }
-#pragma unroll
-    for (int k = 0; k < kSkipWin; k++) {
-      curL[k] = nxtL[k];
-      curE[k] = nxtE[k];
+    } else {
+      const uint32_t L = mlen[p];
+      if (L >= kDictRmqLen) rmq |= !(mdist[p] == 1u && L >= kSameLetter);
     }
   }
-  if (__ballot(rmq) && lane == 0) longFlag[blockIdx.x] = 1u;
+  if (__ballot(rmq) && lane == 0) atomicOr(longFlag + ws.x, 1u);
 }
 
 // the chain tables after the chunk's last insertion, in place (slot s reads only its own carried value)
@@ -381,6 +524,8 @@ __global__ __launch_bounds__(256) void k_dict_carry(DictPlan P, const uint16_t* 
   prevX[s] = x;
 }
 
+uint64_t dict_lz_mask_bytes_per_walk() { return 2 * kLzWords * 4; }
+
 uint64_t dict_sort_keys_max() { return kBlockMaxDict + kWindow + 64; }
 
 uint64_t dict_sort_temp_bytes()
@@ -395,7 +540,8 @@ int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* h
                          uint32_t dictBack, uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH,
                          uint16_t* prevX, uint16_t* ph, uint16_t* pe, uint64_t* keysA, uint64_t* keysB, void* temp,
                          uint64_t tempBytes, uint32_t* gate, uint32_t* mlen, uint16_t* mdist, uint32_t* sel,
-                         uint32_t* longFlag, hipStream_t s)
+                         uint32_t* longFlag, const uint2* walkSegs, uint32_t nwalk, uint32_t* lzMasks, uint4* lzState,
+                         hipStream_t s)
 {
   if (!nb) return 0;
   if (hipMemsetAsync(gate, 0, 4, s)) return -1;
@@ -434,8 +580,13 @@ int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* h
     hipLaunchKernelGGL(k_dict_pe, dim3((maxOwn + 255) / 256, nb), dim3(256), 0, s, in, P, ph, prevH, pe, gate);
   hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 255) / 256, nb), dim3(256), 0, s, in, P, maxChain, pe, prevX, mlen, mdist,
                      sel, longFlag, gate);
-  if (maxChain <= (uint32_t)kLazyMax)
-    hipLaunchKernelGGL(k_dict_skip, dim3(nb), dim3(64), 0, s, dBlocks, pe, mlen, mdist, longFlag, gate);
+  if (maxChain <= (uint32_t)kLazyMax && nwalk) {
+    hipLaunchKernelGGL(k_dict_lz_walk, dim3((nwalk + 3) / 4), dim3(256), 0, s, dBlocks, walkSegs, nwalk, mlen, pe, lzMasks,
+                       lzState, gate);
+    hipLaunchKernelGGL(k_dict_lz_fix, dim3(nb), dim3(64), 0, s, dBlocks, mlen, pe, lzMasks, lzState, gate);
+    hipLaunchKernelGGL(k_dict_lz_clear, dim3((nwalk + 3) / 4), dim3(256), 0, s, dBlocks, walkSegs, nwalk, mlen, mdist, pe,
+                       lzMasks, longFlag, gate);
+  }
   hipLaunchKernelGGL(k_dict_carry, dim3(65536 / 256), dim3(256), 0, s, P, ph, pe, prevH, prevX, gate);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -131,7 +131,7 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
-  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictGate;  // dictionary mode on the whole GPU (sz4_dict.hip)
+  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictGate, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
@@ -179,7 +179,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictGate,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictGate, &dictLz,
             &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
             &unOut, &unSeq};
   }
@@ -369,14 +369,16 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       static const uint64_t tempBytes = dict_sort_temp_bytes();
       if ((e = c->dictPH.reserve(staged * 2)) || (e = c->dictPE.reserve(staged * 2)) ||
           (e = c->dictKeys.reserve(2 * dict_sort_keys_max() * 8)) || (e = c->dictTemp.reserve(tempBytes + 64)) ||
-          (e = c->dictGate.reserve(64)))
+          (e = c->dictGate.reserve(64)) ||
+          (e = c->dictLz.reserve(c->hWalk.size() * dict_lz_mask_bytes_per_walk() + 64)))
         return c->fail(SZ4_E_NOMEM, "dictionary scratch", e);
       if (launch_dict_parallel(in, dB, c->hBlocks.data(), nb, maxChain, (uint32_t)c->dictBack, c->dictCont, c->dictShift,
                                c->dictLow0, c->dictLast.as<uint32_t>(), c->dictPrevH.as<uint16_t>(),
                                c->dictPrevX.as<uint16_t>(), c->dictPH.as<uint16_t>(), c->dictPE.as<uint16_t>(),
                                c->dictKeys.as<uint64_t>(), c->dictKeys.as<uint64_t>() + dict_sort_keys_max(), c->dictTemp.p,
                                tempBytes, c->dictGate.as<uint32_t>(), c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(),
-                               c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s))
+                               c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), c->walkSegs.as<uint2>(),
+                               (uint32_t)c->hWalk.size(), c->dictLz.as<uint32_t>(), c->walkState.as<uint4>(), s))
         return c->fail(SZ4_E_DEVICE, "dictionary kernels");
     }
     mark(c, 2, s);

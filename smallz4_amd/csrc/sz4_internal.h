@@ -120,7 +120,7 @@ void launch_dict_gated(const uint8_t* in, const Block* blocks, uint32_t nblocks,
                        uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, const uint32_t* gate,
                        hipStream_t s);
 // dictionary mode on the whole GPU (sz4_dict.hip), non-legacy frames: hBlocks is the host copy of the
-// plan; ph / pe: one u16 per staged position; keysA / keysB: dict_sort_keys_max() u64 each; temp:
+// plan, walkSegs the token walk's sub-segments; ph / pe: one u16 per staged position; keysA / keysB: dict_sort_keys_max() u64 each; temp:
 // dict_sort_temp_bytes(); gate: one u32.  Returns 0, or -1 on a launch failure
 constexpr uint64_t kBlockMaxDict = 4ull << 20;  // MaxBlockSize (smallz4.h:124)
 uint64_t dict_sort_keys_max();
@@ -129,7 +129,11 @@ int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* h
                          uint32_t dictBack, uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH,
                          uint16_t* prevX, uint16_t* ph, uint16_t* pe, uint64_t* keysA, uint64_t* keysB, void* temp,
                          uint64_t tempBytes, uint32_t* gate, uint32_t* mlen, uint16_t* mdist, uint32_t* sel,
-                         uint32_t* longFlag, hipStream_t s);
+                         uint32_t* longFlag, const uint2* walkSegs, uint32_t nwalk, uint32_t* lzMasks, uint4* lzState,
+                         hipStream_t s);
+// greedy/lazy levels: dict_lz_mask_bytes_per_walk() bytes per token-walk sub-segment (lzMasks), one
+// uint4 per sub-segment (lzState)
+uint64_t dict_lz_mask_bytes_per_walk();
 // k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
 // corrected, run sort/find/prep again
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
