@@ -48,6 +48,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import subprocess
 import sys
 import time
@@ -227,13 +228,20 @@ def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
                               "sample": f"first {done_1 / 1e6:.1f} MB, one thread ({dt_1:.1f} s)"}}
 
 
+def pmc_tag_key(tag: str):
+    """Order of profile tags rNN<suffix>: round, suffix length, suffix."""
+    m = re.match(r"r(\d+)([a-z]*)$", tag)
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, len(tag), tag)
+
+
 def pmc_traffic(cfg):
     """HBM bytes per k_find_sorted launch from the newest profiles/**/*_pmc.json of this workload."""
     best = None
-    # tags run r02a..r02z, r02aa..r02az: order by tag length first so r02av sorts after r02o
+    # tags run r02a..r02z, r02aa..r02az, then r03a..: order by round, then suffix length, then suffix
+    # (so r02av sorts after r02o, and r03a after r02bd)
     paths = glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")) + \
         glob.glob(os.path.join(ROOT, "profiles", "*", "*_pmc.json"))
-    for path in sorted(paths, key=lambda p: (len(os.path.basename(p)), os.path.basename(p))):
+    for path in sorted(paths, key=lambda p: pmc_tag_key(os.path.basename(p)[: -len("_pmc.json")])):
         try:
             with open(path) as f:
                 rec = json.load(f)

@@ -1,21 +1,23 @@
 #!/bin/bash
 # Round-N profile collection on the MI355X box (run from the repo root through gpurun):
-#   bash profiles/collect.sh rNN
+#   bash profiles/collect.sh rNN [bench.py workload args, e.g. --workload silesia]
 # Writes gpurun_out/<tag>/: the bench JSON line, a rocprofv3 kernel-trace --stats summary of the
 # same workload, and separate PMC passes (FETCH_SIZE, WRITE_SIZE, SQ issue counters).  Each GPU
 # step has its own time limit and the chain stops at the first failure.
 set -euo pipefail
 TAG=${1:-r01}
+shift || true
+EXTRA="$*"
 R=${GRAFT_REPO_ROOT:-$PWD}
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-timeout -k 10 400 python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 400 python3 "$R/bench.py" $EXTRA > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp
-ARGS="--steps 10 --warmup 3 --no-verify --no-stream --cpu-seconds 0.5"
+ARGS="--steps 10 --warmup 3 --no-verify --no-stream --no-shapes --cpu-seconds 0.5 $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
   python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1
-ARGS="--steps 3 --warmup 1 --no-verify --no-decode --no-stream --cpu-seconds 0.5"
+ARGS="--steps 3 --warmup 1 --no-verify --no-decode --no-stream --no-shapes --cpu-seconds 0.5 $EXTRA"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o bench -- \
   python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o bench -- \

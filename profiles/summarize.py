@@ -60,6 +60,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
+    ap.add_argument("--workload", default="enwik8")
+    ap.add_argument("--bytes-per-gpu", type=int, default=100_000_000)
+    ap.add_argument("--block-size", type=int, default=65536)
     a = ap.parse_args()
     src = os.path.join(a.src, a.tag)
     stats = os.path.join(src, "trace", "bench_kernel_stats.csv")
@@ -76,7 +79,8 @@ def main():
     def fmt(v, scale=1.0, p=1):
         return "-" if v is None else (f"{v * scale:.{p}f}" if scale != "e" else f"{v:.3g}")
 
-    lines = [f"# {a.tag} kernel profile (bench.py default workload: 100 MB, 64 KiB blocks, -9)", "",
+    lines = [f"# {a.tag} kernel profile (bench.py workload {a.workload}: {a.bytes_per_gpu / 1e6:g} MB, "
+             f"{a.block_size // 1024} KiB blocks, -9)", "",
              f"Source: `bash profiles/collect.sh {a.tag}` on one MI355X, summarised by "
              f"`python profiles/summarize.py {a.tag}` (rocprofv3 --kernel-trace --stats; every PMC pass separate).",
              "FETCH_SIZE doubled per MI355X_MICROARCH.md; MB = 1e6 bytes per launch.", "",
@@ -109,7 +113,8 @@ def main():
         wb = None if wr is None else int(round(wr * 1024))
         cycles = avg_ns * 1e-9 * 2.4e9  # MI355X_MICROARCH.md: 2.4 GHz
         out = {"kernel": "k_find_sorted", "tag": a.tag,
-               "config": {"workload": "enwik8", "bytes_per_gpu": 100_000_000, "block_size": 65536, "level": 9},
+               "config": {"workload": a.workload, "bytes_per_gpu": a.bytes_per_gpu, "block_size": a.block_size,
+                          "level": 9},
                "avg_duration_us": round(avg_ns / 1e3, 1),
                "fetch_bytes_corrected": fb, "write_bytes": wb,
                "hbm_bytes_per_launch": None if fb is None or wb is None else fb + wb,

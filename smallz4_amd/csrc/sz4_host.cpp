@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <mutex>
 #include <cstdio>
 #include <cstring>
@@ -827,25 +828,44 @@ int stream_compress_body(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uin
   if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
   if (have)
     if (int r = upload(1)) return r;
+  // SZ4_STREAM_PROFILE=1: where the caller's thread spends its time, per phase, on stderr
+  const bool prof = getenv("SZ4_STREAM_PROFILE") != nullptr;
+  double tp[6] = {0, 0, 0, 0, 0, 0};
+  auto now = []() { return std::chrono::steady_clock::now(); };
+  auto lap = [&](std::chrono::steady_clock::time_point& t, int i) {
+    const auto u = now();
+    tp[i] += std::chrono::duration<double>(u - t).count();
+    t = u;
+  };
   for (uint32_t k = 0;; k++) {
     const uint32_t sl = k & 1;
     uint64_t size = 0;
+    auto t = now();
     if (int r = finish(k, &size)) return r;
+    lap(t, 0);
     if (have)
       if (int r = compute(k + 1)) return r;  // the GPU goes on with chunk k+1 ...
+    lap(t, 1);
     // ... while chunk k comes down and goes out, and chunk k+2 is read and goes up
     if ((e = grow_pinned(c->hostOut[sl], std::max<uint64_t>(size, 1), 0))) return c->fail(SZ4_E_NOMEM, "pinned host buffers", e);
     if ((e = hipMemcpyAsync(c->hostOut[sl].p, c->chunkOut[sl].p, size, hipMemcpyDeviceToHost, c->downStream)) ||
         (e = hipStreamSynchronize(c->downStream)))
       return c->fail(SZ4_E_DEVICE, "download", e);
+    lap(t, 2);
     send_blocks(c->hostOut[sl].as<uint8_t>(), size, send, out);
+    lap(t, 3);
     if (!have) break;
     have = next_chunk(k + 2);
     if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
     if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
+    lap(t, 4);
     if (have)
       if (int r = upload(k + 2)) return r;
+    lap(t, 5);
   }
+  if (prof)
+    fprintf(stderr, "sz4 stream: finish-wait %.3f s, enqueue %.3f s, download %.3f s, sendBytes %.3f s, getBytes %.3f s, "
+            "upload-enqueue %.3f s\n", tp[0], tp[1], tp[2], tp[3], tp[4], tp[5]);
   if (!legacy) {
     static const uint8_t zero[4] = {0, 0, 0, 0};
     send(zero, 4, out);  // end mark (smallz4.h:807-812)

@@ -757,6 +757,10 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 #define SZ4_LPF_LONG 0
 #endif
 constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
+#ifndef SZ4_LPF_SLACK
+#define SZ4_LPF_SLACK 2
+#endif
+constexpr uint32_t kLpfSlack = SZ4_LPF_SLACK;  // probes that may have another preceding byte
 template <class Src>
 __device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint32_t gs, uint32_t slot, uint32_t cls,
                                            uint64_t w0, uint64_t predLo, uint32_t me1, uint32_t me2, const Src& src)
@@ -767,7 +771,7 @@ __device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint
     same += q > predLo && (src.ld4(q - 1) & 0xFFu) == cls ? 1u : 0u;
     if constexpr (kLpfLong > 0) longer += src.ld4(q + 4) == me1 && src.ld4(q + 8) == me2 ? 1u : 0u;
   }
-  return same + 2u >= kLpfProbe && longer >= kLpfLong;
+  return same + kLpfSlack >= kLpfProbe && longer >= kLpfLong;
 }
 
 template <bool kLds>

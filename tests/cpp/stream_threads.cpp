@@ -69,10 +69,17 @@ struct Big {
   uint64_t reps, pos, total;
   FILE* out;
   uint64_t sent;
+  double getSecs, sendSecs;  // time spent inside the callbacks (the caller's side of the interface)
+};
+struct CallbackClock {
+  double* acc;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  ~CallbackClock() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); }
 };
 size_t get_big(void* data, size_t n, void* user)
 {
   Big* b = static_cast<Big*>(user);
+  CallbackClock clock{&b->getSecs};
   unsigned char* d = static_cast<unsigned char*>(data);
   const uint64_t size = b->base->size();
   size_t k = 0;
@@ -94,6 +101,7 @@ size_t get_big(void* data, size_t n, void* user)
 void send_big(const void* data, size_t n, void* user)
 {
   Big* b = static_cast<Big*>(user);
+  CallbackClock clock{&b->sendSecs};
   if (n) fwrite(data, 1, n, b->out);
   b->sent += n;
 }
@@ -123,7 +131,7 @@ int main(int argc, char** argv)
   }
   if (std::string(argv[1]) == "big" && argc >= 6) {
     std::vector<unsigned char> base = read_file(argv[3]);
-    Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, fopen(argv[5], "wb"), 0};
+    Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, fopen(argv[5], "wb"), 0, 0.0, 0.0};
     b.total = b.reps * base.size();
     const auto t0 = std::chrono::steady_clock::now();
     smallz4::lz4(get_big, send_big, chain, false, &b);
@@ -132,9 +140,10 @@ int main(int argc, char** argv)
     // the footprint of the pooled context the call used (handed back to the pool, borrowed again)
     sz4_ctx* c = NULL;
     sz4_acquire(&c, getenv("SMALLZ4_AMD_DEVICE") ? atoi(getenv("SMALLZ4_AMD_DEVICE")) : 0);
-    printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu, \"seconds\": %.3f, \"MB/s\": %.1f}\n",
+    printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu, \"seconds\": %.3f, \"MB/s\": %.1f, "
+           "\"get_bytes_seconds\": %.3f, \"send_bytes_seconds\": %.3f}\n",
            (unsigned long long)b.total, (unsigned long long)b.sent, (unsigned long long)sz4_device_bytes(c), secs,
-           b.total / secs / 1e6);
+           b.total / secs / 1e6, b.getSecs, b.sendSecs);
     sz4_release(c);
     return 0;
   }

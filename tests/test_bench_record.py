@@ -1,6 +1,7 @@
 """CPU checks of the bench line's provenance: the roofline's `traffic` and issue rates come from the
-newest committed PMC summary of the same workload (profiles/<tag>_pmc.json), tags ordered r02a..r02z,
-r02aa..r02az, ... (a plain string sort would put r02o after r02bd)."""
+newest committed PMC summary of the same workload (profiles/<tag>_pmc.json), tags ordered by round, then
+r02a..r02z, r02aa..r02az, ... (a plain string sort would put r02o after r02bd, a length sort r03a before
+r02bd)."""
 import json
 import os
 import sys
@@ -14,7 +15,12 @@ DEFAULT_CFG = {"workload": "enwik8", "bytes_per_gpu": 100_000_000, "block_size":
 
 
 def _tag_key(tag):
-    return (len(tag), tag)
+    return bench.pmc_tag_key(tag)
+
+
+def test_tag_order():
+    tags = ["r02o", "r02bd", "r03a", "r02av", "r03ab", "r03z", "r01h"]
+    assert sorted(tags, key=_tag_key) == ["r01h", "r02o", "r02av", "r02bd", "r03a", "r03z", "r03ab"]
 
 
 def test_pmc_traffic_takes_newest_tag_of_the_workload():
