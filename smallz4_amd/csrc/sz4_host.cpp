@@ -846,22 +846,26 @@ int stream_compress_body(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uin
     if (have)
       if (int r = compute(k + 1)) return r;  // the GPU goes on with chunk k+1 ...
     lap(t, 1);
-    // ... while chunk k comes down and goes out, and chunk k+2 is read and goes up
+    // ... while chunk k comes down (its copy overlaps the read of chunk k+2) and goes out, and chunk
+    // k+2 is read and goes up
     if ((e = grow_pinned(c->hostOut[sl], std::max<uint64_t>(size, 1), 0))) return c->fail(SZ4_E_NOMEM, "pinned host buffers", e);
-    if ((e = hipMemcpyAsync(c->hostOut[sl].p, c->chunkOut[sl].p, size, hipMemcpyDeviceToHost, c->downStream)) ||
-        (e = hipStreamSynchronize(c->downStream)))
+    if ((e = hipMemcpyAsync(c->hostOut[sl].p, c->chunkOut[sl].p, size, hipMemcpyDeviceToHost, c->downStream)))
       return c->fail(SZ4_E_DEVICE, "download", e);
+    const bool more = have;
+    if (more) {
+      have = next_chunk(k + 2);
+      if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
+      if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
+      lap(t, 4);
+      if (have)
+        if (int r = upload(k + 2)) return r;
+      lap(t, 5);
+    }
+    if ((e = hipStreamSynchronize(c->downStream))) return c->fail(SZ4_E_DEVICE, "download", e);
     lap(t, 2);
     send_blocks(c->hostOut[sl].as<uint8_t>(), size, send, out);
     lap(t, 3);
-    if (!have) break;
-    have = next_chunk(k + 2);
-    if (he) return c->fail(SZ4_E_NOMEM, "pinned host buffers", he);
-    if (bad) return c->fail(SZ4_E_ARG, "getBytes returned more bytes than asked for");
-    lap(t, 4);
-    if (have)
-      if (int r = upload(k + 2)) return r;
-    lap(t, 5);
+    if (!more) break;
   }
   if (prof)
     fprintf(stderr, "sz4 stream: finish-wait %.3f s, enqueue %.3f s, download %.3f s, sendBytes %.3f s, getBytes %.3f s, "

@@ -758,7 +758,7 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 #endif
 constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
 #ifndef SZ4_LPF_SLACK
-#define SZ4_LPF_SLACK 2
+#define SZ4_LPF_SLACK 1
 #endif
 constexpr uint32_t kLpfSlack = SZ4_LPF_SLACK;  // probes that may have another preceding byte
 template <class Src>

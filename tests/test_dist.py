@@ -84,6 +84,11 @@ def test_bench_gpus2_dry_run_starts_two_ranks():
         rec = json.loads(line)
         assert rec["n_gpus"] == 2 and rec["dry_run"] and rec["parts_equal_single"], rec
         assert rec["input_bytes"] == 2 * int(mb * 1e6)
+        # the N > 1 line carries what north_star asks at every N: the workload (the same one the N=1
+        # shapes leg runs for configs[3]), the host-CPU baseline with its core count, a bounded verify leg
+        assert rec["workload"] == workload
+        assert rec["cpu_baseline"]["value"] > 0 and rec["cpu_baseline"]["cores"] >= 1, rec["cpu_baseline"]
+        assert 0 < rec["verify_budget_s"] <= 60
 
 
 def test_range_generators_are_slices_of_one_input():
