@@ -62,6 +62,9 @@
 #else
 #define SZ4_HBM_SGPR 96
 #endif
+#ifndef SZ4_XCD_ORDER  // k_find_sorted_hbm: contiguous runs of segments per XCD (A/B: no gain, profiles/r03/r03j2)
+#define SZ4_XCD_ORDER 0
+#endif
 #ifndef SZ4_DIAG
 #define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
 #endif
@@ -774,6 +777,15 @@ __device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint
   return same + kLpfSlack >= kLpfProbe && longer >= kLpfLong;
 }
 
+// workgroup i runs on XCD i mod 8 (observed, for speed only): XCD x's k-th workgroup takes segment
+// start(x) + k, so each XCD walks one contiguous run of segments
+__device__ __forceinline__ uint32_t xcd_segment(uint32_t i, uint32_t n)
+{
+  constexpr uint32_t kXcd = 8;
+  const uint32_t per = n / kXcd, extra = n % kXcd, x = i % kXcd, k = i / kXcd;
+  return x * per + (x < extra ? x : extra) + k;
+}
+
 template <bool kLds>
 __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                 const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
@@ -793,7 +805,11 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #if SZ4_DIAG == 3
   const uint64_t tEntry = __builtin_readcyclecounter();
 #endif
-  const Segment S = segs[blockIdx.x];
+  // blocks above 64 KiB: consecutive segments of a block share 64 KiB of window and their text comes
+  // from HBM/L2 -- give each XCD a contiguous run of segments (workgroups are dealt round-robin over
+  // the 8 XCDs, MI355X_MICROARCH.md "Workgroup dispatch"), so the runs stay in that XCD's L2
+  const uint32_t segIdx = (kLds || !SZ4_XCD_ORDER) ? blockIdx.x : xcd_segment(blockIdx.x, gridDim.x);
+  const Segment S = segs[segIdx];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t waveId = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
@@ -1441,7 +1457,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   const uint64_t tSearch = __builtin_readcyclecounter();
 #endif
   __syncthreads();
-  if (tid == 0) segLong[blockIdx.x] = s_long;
+  if (tid == 0) segLong[segIdx] = s_long;
 
   // results in text order: tile by tile, the bucket is scattered into LDS (the window is free now)
   // and written out coalesced -- mlen u32, mdist u16 and pass 2's marker bits.  Targets no bucket
@@ -4843,30 +4859,39 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   xL1 = ldw(a + 64);
   xL2 = ldw(a + 128);
   xL3 = ldw(a + 192);
+  // per window, each lane's offset of the first match at or after it (64: none): computed once per
+  // window on the vector unit, so a step of the walk is two readlanes instead of a ballot and a bit scan
+  auto next_match = [&]() -> uint32_t {
+    const uint64_t ge = __ballot(wL > 1u && wbase + lane < n) & (~0ull << lane);
+    return ge ? (uint32_t)__builtin_ctzll(ge) : 64u;
+  };
+  uint32_t nm = next_match();
   while (pos < aNext) {
-    while (pos >= wbase + 64) {
-      if (pos < wbase + 256) {
-        wbase += 64;
-        wL = xL1;
-        xL1 = xL2;
-        xL2 = xL3;
-        xL3 = ldw(wbase + 192);
-      } else {
-        wbase = pos & ~63u;
-        wL = ldw(wbase);
-        xL1 = ldw(wbase + 64);
-        xL2 = ldw(wbase + 128);
-        xL3 = ldw(wbase + 192);
+    if (pos >= wbase + 64) {
+      while (pos >= wbase + 64) {
+        if (pos < wbase + 256) {
+          wbase += 64;
+          wL = xL1;
+          xL1 = xL2;
+          xL2 = xL3;
+          xL3 = ldw(wbase + 192);
+        } else {
+          wbase = pos & ~63u;
+          wL = ldw(wbase);
+          xL1 = ldw(wbase + 64);
+          xL2 = ldw(wbase + 128);
+          xL3 = ldw(wbase + 192);
+        }
       }
+      nm = next_match();
     }
-    const uint32_t rel = pos - wbase;
-    const uint64_t mm = __ballot(wL > 1u && wbase + lane < n) & (~0ull << rel);
-    const uint32_t q = mm ? wbase + (uint32_t)__builtin_ctzll(mm) : wbase + 64;  // next match (or window end)
+    const uint32_t qr = rdlane(nm, pos - wbase);
+    const uint32_t q = wbase + qr;  // next match (or window end)
     if (q >= aNext) {
       viaMatch = false;  // literals carry the path to aNext itself
       break;
     }
-    if (mm == 0) {
+    if (qr == 64u) {
       pos = q;
       viaMatch = false;
       continue;
@@ -4880,7 +4905,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
     slotBuf = wrlane(slotBuf, q, m & 63u);
     m++;
     if ((m & 63u) == 0u) slots[m - 64u + lane] = slotBuf;
-    pos = q + rdlane(wL, q - wbase);
+    pos = q + rdlane(wL, qr);
     viaMatch = true;
   }
   if (lane < (m & 63u)) slots[(m & ~63u) + lane] = slotBuf;
