@@ -2510,8 +2510,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
     const uint32_t ga = s_groups[2 * gi], gb = s_groups[2 * gi + 1];
     // the group's run key, if it has one (its first or last member's; other keys in the group are
     // 16-bit hash collisions, handled one by one below)
+    // (the first and last members can both be collisions -- a random position that hashes like the
+    // run key -- so members spread over the group are sampled too; s_mixed below weighs the rest)
     uint32_t gKey = gload4(in, S.w0 + slot_pos(compact, small, ga));
-    if (!run_key(gKey)) gKey = gload4(in, S.w0 + slot_pos(compact, small, gb - 1));
+    for (uint32_t k = 1; k <= 8 && !run_key(gKey); k++) {
+      const uint32_t at = k == 8 ? gb - 1 : ga + (uint32_t)((uint64_t)(gb - ga) * k / 8);
+      gKey = gload4(in, S.w0 + slot_pos(compact, small, at));
+    }
     if (tid == 0) s_mixed = 0;
     __syncthreads();
     if (run_key(gKey)) {

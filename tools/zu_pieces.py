@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: configs[4]'s rank-0 slice (zeros/urandom, 256 KiB blocks) compressed piece by piece, to
-find the regions whose find_long stage is slow.  python tools/zu_pieces.py [piece MiB] [total MiB]"""
+find the regions whose find_long stage is slow.  python tools/zu_pieces.py [piece MiB] [end MiB] [start MiB]"""
 import json
 import os
 import sys
@@ -16,10 +16,11 @@ from smallz4_amd import synth  # noqa: E402
 
 piece = int(float(sys.argv[1]) * (1 << 20)) if len(sys.argv) > 1 else 256 << 20
 total = int(float(sys.argv[2]) * (1 << 20)) if len(sys.argv) > 2 else 1280 << 20
+start = int(float(sys.argv[3]) * (1 << 20)) if len(sys.argv) > 3 else 0
 bs = 262144
 comp = smallz4_amd.Compressor(device=0)
 comp.set_timing(True)
-for lo in range(0, total, piece):
+for lo in range(start, total, piece):
     hi = min(lo + piece, total)
     data = synth.zeros_urandom_range(lo, hi, seed=10)
     x = np.frombuffer(data, dtype=np.uint8)
@@ -36,7 +37,7 @@ for lo in range(0, total, piece):
     z = np.concatenate(([0], (x == 0).astype(np.int8), [0]))
     d = np.diff(z)
     runs = np.flatnonzero(d == -1) - np.flatnonzero(d == 1)
-    print(json.dumps({"lo_MiB": lo >> 20, "hi_MiB": hi >> 20, "ms": round(dt * 1e3, 2),
+    print(json.dumps({"lo_MiB": lo / (1 << 20), "hi_MiB": hi / (1 << 20), "ms": round(dt * 1e3, 2),
                       "stages_ms": {k: round(v, 2) for k, v in comp.last_stage_ms().items()},
                       "zero_runs": int(len(runs)), "max_zero_run": int(runs.max()) if len(runs) else 0,
                       "runs_over_256k": int((runs > bs).sum())}), flush=True)
