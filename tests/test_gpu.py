@@ -104,6 +104,24 @@ def test_blocks_structured_content(compressor, kind, bs):
         assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain), chain
 
 
+def test_zero_run_group_with_collision_ends(compressor):
+    """A configs[4] block whose zero-run key group starts and ends with 16-bit hash collisions (random
+    positions that hash like 0x00000000): k_find_big must still take it as a run-key group.  Round 3
+    sent it to the class path (550 ms for one block, byte-identical but 700x slower); the oracle decides
+    the bytes, the stage clock the path."""
+    bs = 262144
+    lo = 334495744  # 319 MiB into configs[4]'s rank-0 slice
+    data = synth.zeros_urandom_range(lo, lo + bs, seed=10)
+    compressor.set_timing(True)
+    try:
+        frame = compressor.compress_blocks(data, bs, 65535)
+        find_long = compressor.last_stage_ms()["find_long"]
+    finally:
+        compressor.set_timing(False)
+    assert frame[7:-4] == pyoracle.oz_block(data, 65535)
+    assert find_long < 50.0, find_long
+
+
 def test_blocks_silesia_mix_4m(compressor):
     """configs[2]'s shape: Silesia-shaped mixed content in 4 MiB independent blocks."""
     data = synth.silesia_like(5 << 20, seed=78)

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Diagnostic: compress one saved 256 KiB block (tools/zu_slow_block.bin) a few times with stage times;
+"""Diagnostic: compress one 256 KiB block of configs[4]'s generator (at 319 MiB: its zero-run group
+starts and ends with hash collisions) a few times with stage times;
 with SMALLZ4_AMD_LIB pointing at a SZ4_DIAG=6 build also k_find_big's counters."""
 import ctypes
 import json
@@ -14,7 +15,9 @@ import torch  # noqa: E402,F401
 import smallz4_amd  # noqa: E402
 from oracle import pyoracle  # noqa: E402  (checker)
 
-data = open(os.path.join(ROOT, "tools", "zu_slow_block.bin"), "rb").read()
+from smallz4_amd import synth  # noqa: E402
+
+data = synth.zeros_urandom_range(334495744, 334495744 + 262144, seed=10)
 comp = smallz4_amd.Compressor()
 comp.set_timing(True)
 diag = "diag" in os.environ.get("SMALLZ4_AMD_LIB", "")
