@@ -150,16 +150,89 @@ def parallel(data, blocks, dictBack, maxChain):
     cX = [read_slot(pe, s, b, it) for s in range(65536)]
     return mlen, mdist, cH, cX
 
-for (bs, n, dl, chain, seed) in [(131072, 300000, 20000, 65535, 1), (65536*2, 280000, 65535, 5, 2), (65536*3, 200000, 3000, 65535, 3)]:
+
+# ---- greedy/lazy bookkeeping (k_dict_lz_walk / _fix / _clear): the speculative per-sub-segment walk
+# against the reference's serial skip loop (smallz4.h:726-744), on linked flags and lengths
+def lz_serial(linked, L):
+    kept=set(); skip=0; lazy=False
+    for q in range(len(L)):
+        if not linked[q]: continue
+        if skip>0:
+            skip-=1
+            if not lazy: continue
+            lazy=False
+        kept.add(q)
+        if L[q]!=1:
+            lazy = skip==0; skip=L[q]
+    return kept
+def lz_next(linked, pos, need):
+    while pos < len(linked):
+        if linked[pos]:
+            if need==0: return pos
+            need-=1
+        pos+=1
+    return 10**9
+def lz_step(linked,L,q,md,carry):
+    if md==0:
+        if L[q]!=1: carry=L[q]-1; md=1
+        return lz_next(linked,q+1,0),md,carry
+    return lz_next(linked,q+1,L[q] if L[q]!=1 else carry),0,carry
+def lz_spec(linked, L, SEG=64):
+    n=len(L); segs=[]
+    for a in range(0,n,SEG):
+        an=min(a+SEG,n); fresh=set(); kept=set(); md=0; carry=0
+        q=lz_next(linked,a,0)
+        while q<an:
+            kept.add(q)
+            if md==0: fresh.add(q)
+            q,md,carry=lz_step(linked,L,q,md,carry)
+        segs.append([fresh,kept,(q,md,carry)])
+    ex=segs[0][2]
+    for k in range(1,len(segs)):
+        a=k*SEG; an=min(a+SEG,n); fresh,kept,sp=segs[k]
+        q,md,carry=ex
+        if q>=an: segs[k][1]=set(); continue
+        merged = md==0 and q in fresh; rep=set()
+        if not merged:
+            while q<an:
+                if md==0 and q in fresh: merged=True; break
+                rep.add(q); q,md,carry=lz_step(linked,L,q,md,carry)
+        frm = q if merged else an
+        segs[k][1]=rep|{x for x in kept if x>=frm}
+        ex = sp if merged else (q,md,carry)
+    out=set()
+    for s in segs: out|=s[1]
+    return out
+
+
+def make_case(bs, n, dl, seed):
     dic = synth.enwik8_like(dl, seed=seed)
-    body = synth.enwik8_like(n, seed=seed+10)
+    body = synth.enwik8_like(n, seed=seed + 10)
     dictBack = min(dl, W)
     prefix = (b'\0' * W + dic)[-W:]
     data = prefix + body + b'\0' * 16
     blocks = []
     s = W
     while s < W + n:
-        blocks.append((s, min(s + bs, W + n))); s += bs
-    a = serial(data, blocks, dictBack, chain)
-    b = parallel(data, blocks, dictBack, chain)
-    print(bs, n, dl, chain, 'mlen', a[0] == b[0], 'mdist', a[1] == b[1], 'prevH', a[2] == b[2], 'prevX', a[3] == b[3], len(a[0]))
+        blocks.append((s, min(s + bs, W + n)))
+        s += bs
+    return data, blocks, dictBack
+
+
+if __name__ == "__main__":
+    import random
+    random.seed(1)
+    for t in range(3000):
+        n = random.randint(1, 700)
+        p = random.random()
+        linked = [random.random() < p for _ in range(n)]
+        L = [random.choice([1, 1, 2, 3, 4, 5, 6, 9, 20, 100]) for _ in range(n)]
+        assert lz_serial(linked, L) == lz_spec(linked, L), (t, n)
+    print("lazy walk: 3000 random cases equal")
+    for (bs, n, dl, chain, seed) in [(131072, 300000, 20000, 65535, 1), (65536 * 2, 280000, 65535, 5, 2),
+                                     (65536 * 3, 200000, 3000, 65535, 3)]:
+        data, blocks, dictBack = make_case(bs, n, dl, seed)
+        a = serial(data, blocks, dictBack, chain)
+        b = parallel(data, blocks, dictBack, chain)
+        print(bs, n, dl, chain, 'mlen', a[0] == b[0], 'mdist', a[1] == b[1], 'prevH', a[2] == b[2], 'prevX', a[3] == b[3],
+              len(a[0]))
