@@ -34,8 +34,9 @@ Also reported:
   roundtrip      every rank's part decoded on the device (sz4_unlz4_device) equals its input
   roofline       dominant kernel (k_find_sorted), HIP-event timed on its stream; HBM traffic from the
                  newest matching profiles/*_pmc.json (rocprofv3 PMC passes of the same workload)
-  cpu_baseline   the reference itself on this host (rank 0, every N, after the timed region): all 16
-                 host threads of the box's share, and one thread, on a bounded sample
+  cpu_baseline   the reference itself on this host (rank 0, every N, after the timed region): one
+                 thread per CPU this process may use (affinity mask, capped by the cgroup quota; the
+                 count is recorded), and one thread, on a bounded sample
   stream         sz4_lz4 (the drop-in's host-buffer path: 4 MiB dependent blocks, chunked, PCIe
                  included) between numpy buffers, 1 GPU, outside the timed region
   shapes         N=1: the other single-GPU-sized configs -- configs[2] (Silesia-shaped, 4 MiB blocks),
@@ -63,7 +64,28 @@ METRIC = "input MB/s at -9 optimal parse; output-byte diff vs smallz4 (must be 0
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 CLOCK_GHZ = 2.4         # MI355X_MICROARCH.md: max clock
 SIMDS, CUS = 1024, 256  # 256 CUs x 4 SIMDs
-HOST_THREADS = 16       # the GPU box's CPU share per GPU (gpurun) -- the all-cores baseline
+
+
+def host_cpus():
+    """(threads the CPU baseline runs on, how they were found): the CPUs this process may run on
+    (sched_getaffinity), lowered to the cgroup CPU quota when one is set (cpu.max: a quota limits
+    throughput without shrinking the affinity mask)."""
+    n = len(os.sched_getaffinity(0))
+    src = f"sched_getaffinity: {n}"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            src += f", cgroup cpu.max quota: {q}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, src
+
+
+HOST_THREADS, HOST_THREADS_SOURCE = host_cpus()
+POOL = min(HOST_THREADS, 16)  # generator processes and reference-diff workers (the box's share per GPU)
 
 # name -> (BASELINE config, description, block size, bytes per rank at N ranks, range generator)
 WORKLOADS = {
@@ -72,14 +94,14 @@ WORKLOADS = {
                lambda lo, hi: synth.enwik8_like(100_000_000, seed=8)[lo:hi]),
     "enwik9": ("configs[3]", "synthetic enwik9-shaped text: 16 MiB enwik8-shaped segments (synth.enwik9_like_range)",
                65536, lambda world: 125_000_000,
-               lambda lo, hi: synth.enwik9_like_range(lo, hi, seed=9, workers=HOST_THREADS)),
+               lambda lo, hi: synth.enwik9_like_range(lo, hi, seed=9, workers=POOL)),
     "zeros_urandom": ("configs[4]", "synthetic: zero and urandom runs of random lengths, mean 128 KiB, 50/50 bytes "
                                     "(synth.zeros_urandom_range)",
                       262144, lambda world: (10 << 30) // 8,
                       lambda lo, hi: synth.zeros_urandom_range(lo, hi, seed=10)),
     "silesia": ("configs[2]", "synthetic Silesia-shaped mixed content (synth.silesia_like; the corpus is not available offline)",
                 4 << 20, lambda world: 211_938_580,
-                lambda lo, hi: synth.silesia_like(hi, seed=2, workers=HOST_THREADS)[lo:hi]),
+                lambda lo, hi: synth.silesia_like(hi, seed=2, workers=POOL)[lo:hi]),
     # diagnostic shapes (not BASELINE configs): the kernels' floors on incompressible / all-run data
     "random": ("diagnostic", "synthetic: urandom bytes (numpy, seeded)", 65536, lambda world: 100_000_000,
                lambda lo, hi: synth.random_bytes(hi, seed=8)[lo:hi]),
@@ -103,7 +125,7 @@ def parse_args(argv=None):
     ap.add_argument("--block-size", type=int, default=None, help="override the workload's block size")
     ap.add_argument("--level", type=int, default=9)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of each CPU baseline sample")
-    ap.add_argument("--verify-threads", type=int, default=HOST_THREADS)
+    ap.add_argument("--verify-threads", type=int, default=POOL)
     ap.add_argument("--verify-seconds", type=float, default=20.0,
                     help="per-rank budget of the sampled byte diff against the reference (the whole "
                          "input at N=1 on enwik8 is always diffed)")
@@ -192,9 +214,17 @@ def verify_sample(part: bytes, data: bytes, bs: int, chain: int, threads: int, b
                 m = min(len(got), len(want))
                 diff += sum(1 for a, b in zip(got[:m], want[:m]) if a != b) + abs(len(got) - len(want))
             done += 1
-    return {"byte_diff": diff, "blocks_verified": done, "blocks_total": nblk, "verified_against": kind,
+    complete = done == nblk
+    if every and not complete:
+        sample = f"every block requested, {nblk - done} not diffed (reference timeout or budget): incomplete"
+    elif every:
+        sample = "every block"
+    else:
+        sample = "seeded random order, cut at the budget"
+    return {"byte_diff": diff if (complete or not every) else -1, "byte_diff_of_verified": diff,
+            "blocks_verified": done, "blocks_total": nblk, "verified_against": kind, "verify_complete": complete,
             "verify_seconds": round(time.perf_counter() - t0, 2), "verify_budget_s": budget_s,
-            "verify_sample": "every block" if every else "seeded random order, cut at the budget"}
+            "verify_sample": sample}
 
 
 def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
@@ -221,7 +251,8 @@ def cpu_baseline(data: bytes, bs: int, chain: int, budget_s: float):
 
     done_n, dt_n = run(HOST_THREADS)
     done_1, dt_1 = run(1)
-    return {"value": round(done_n / dt_n / 1e6, 3), "unit": "MB/s", "cores": HOST_THREADS, "kind": kind,
+    return {"value": round(done_n / dt_n / 1e6, 3), "unit": "MB/s", "cores": HOST_THREADS,
+            "cores_source": HOST_THREADS_SOURCE, "kind": kind,
             "sample": f"first {done_n / 1e6:.1f} MB of the rank-0 shard as {bs}-byte blocks, maxChainLength {chain}, "
                       f"smallz4::lz4 per block on {HOST_THREADS} threads ({dt_n:.1f} s)",
             "single_thread": {"value": round(done_1 / dt_1 / 1e6, 3), "cores": 1,

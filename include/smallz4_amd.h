@@ -174,6 +174,11 @@ int sz4_unlz4_stream(sz4_ctx* ctx, sz4_get_byte get_byte, sz4_send_out send_byte
 /* Device memory (bytes) the context holds: its grow-only scratch, staging and output buffers. */
 uint64_t sz4_device_bytes(sz4_ctx* ctx);
 
+/* Dictionary mode: match-finder rounds the last chunk took (the data-parallel finder assumes the
+ * same-letter shortcut intervals and reruns a chunk whose results imply others; 1 = none to correct,
+ * 0 = no dictionary chunk yet, UINT32_MAX = the chunk fell back to the in-order replay). */
+uint32_t sz4_dict_rounds(sz4_ctx* ctx);
+
 /* Last error message of the context ("" if none). */
 const char* sz4_last_error(sz4_ctx* ctx);
 

@@ -89,7 +89,10 @@ class Compressor:
         """sz4_lz4 between caller-owned host buffers (numpy uint8 arrays, no Python copies): compresses
         src into dst (at least sz4_lz4_bound(len(src)) bytes) and returns the frame length."""
         import numpy as np
-        src = np.ascontiguousarray(src, dtype=np.uint8)
+        if isinstance(src, np.ndarray):
+            src = np.ascontiguousarray(src, dtype=np.uint8)
+        else:  # bytes-like: wrapped without a copy (read-only is fine, the library only reads it)
+            src = np.frombuffer(memoryview(src).cast("B"), dtype=np.uint8)
         if not (isinstance(dst, np.ndarray) and dst.dtype == np.uint8 and dst.flags.c_contiguous):
             raise TypeError("dst must be a contiguous numpy uint8 array")
         size = ctypes.c_uint64()
@@ -246,6 +249,11 @@ class Compressor:
     def device_bytes(self) -> int:
         """Device memory held by this context (scratch, staging, output buffers)."""
         return int(self._lib.sz4_device_bytes(self._h))
+
+    def dict_rounds(self) -> int:
+        """Dictionary mode: match-finder rounds of the last chunk (sz4_dict_rounds; 0xFFFFFFFF: the
+        chunk fell back to the in-order replay)."""
+        return int(self._lib.sz4_dict_rounds(self._h))
 
     def set_timing(self, on: bool):
         self._lib.sz4_set_timing(self._h, int(on))

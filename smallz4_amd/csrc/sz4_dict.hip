@@ -12,23 +12,28 @@
 //     the arrays of every position's previousHash / previousExact;
 //   * previousExact (smallz4.h:668-720) is the hash-chain walk over those snapshot reads, and
 //     findLongestMatch (smallz4.h:173-255) the exact-chain walk over them: one lane per position.
-// The same-letter shortcut (smallz4.h:631-643) would make the set of inserted positions depend on the
-// matches; it needs a distance-1 match longer than MaxSameLetter, i.e. a run of more than 65 300 equal
-// bytes inside a block.  k_dict_detect flags a chunk that has a uniform aligned 32 KiB window inside
-// its blocks (a superset of those runs) and such a chunk takes the reference loop replayed in order
-// (k_dict_matches in sz4_kernels.hip), as do legacy frames.
+// The same-letter shortcut (smallz4.h:631-643) makes the set of inserted positions depend on the
+// matches: a position after a distance-1 match longer than MaxSameLetter is neither inserted nor
+// searched and copies that match one byte shorter.  The kernels take an ASSUMED set of shortcut
+// intervals per block (the plan's interval lists), and k_dict_sc_bits / k_dict_sc derive from the
+// results the intervals the reference's loop would take; where they differ the host runs the chunk
+// again from its saved tables with the derived set.  Up to the first disagreement both sets are equal,
+// and at it the derived one is right (its prefix was computed from the reference's state), so every
+// round confirms a longer prefix and the rounds end (tools/dict_model.py model-checks this).
+// Legacy frames (smallz4.h:806-817 resets the tables after every block, and nothing is inserted before
+// a block, lookback 0) are the same computation with independent blocks.
 //
 //   k_dict_begin    the carried tables: reset (first chunk) or shifted with the staged coordinates
-//   k_dict_detect   the fallback gate above
-//   k_dict_keys     per block: (hash << 23 | position) of its own insertions and the 64 KiB before them
+//   k_dict_keys     per block: (hash << 23 | position) of its own insertions (shortcut positions last)
 //   (rocPRIM radix sort of the keys)
 //   k_dict_ph       previousHash of every insertion: its predecessor in the sorted run of its hash
 //   k_dict_last     the hash table's final positions (lastHash, smallz4.h:650-652)
 //   k_dict_pe       previousExact of every insertion: the hash-chain walk over snapshot reads
-//   k_dict_search   findLongestMatch of every linked position of every block
+//   k_dict_search   findLongestMatch of every linked position of every block; shortcut positions copy
 //   k_dict_lz_*     greedy/lazy levels: the reference's skip bookkeeping (smallz4.h:726-744), walked
 //                   speculatively per 4096-position sub-segment and repaired per block
 //   k_dict_carry    the final chain tables, for the next chunk
+//   k_dict_sc_bits, k_dict_sc   the shortcut intervals the results imply, compared with the assumed ones
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -44,56 +49,88 @@ namespace sz4 {
 constexpr uint32_t kDictNoPos = 0xFFFFFFFFu;
 constexpr uint32_t kDictPosBits = 23;  // a block's insertions and the 64 KiB below them: < 2^23 positions
 constexpr uint64_t kDictPosMask = (1ull << kDictPosBits) - 1;
-constexpr uint32_t kDictRmqLen = 274;  // as kRmqLen in sz4_kernels.hip: the parse's range-minimum flag
+constexpr uint32_t kDictSkipKey = 1u << kHashBits;  // k_dict_keys: a shortcut position (sorts after every hash)
+constexpr uint32_t kDictSortBits = kHashBits + 1 + kDictPosBits;
 
 // the insertion steps of one chunk: block b inserts block-relative i = back(b) .. size - 12
-// (smallz4.h:612-625, 627); every block but the stream's first re-inserts the previous block's last
-// 12 positions, and the first of them (i = -12) was that block's last insertion: a duplicate whose
-// entries are both EndOfChain (its lastHash is itself, distance 0)
+// (smallz4.h:612-625, 627) minus its shortcut intervals; every block but the stream's first re-inserts
+// the previous block's last 12 positions, and the first of them (i = -12) was that block's last
+// insertion: a duplicate whose entries are both EndOfChain (its lastHash is itself, distance 0).
+// Legacy frames insert nothing before a block (lookback 0) and start every block from empty tables.
 struct DictPlan {
   const Block* blocks;
   uint32_t nb;
   uint32_t cont;      // the first block continues the previous chunk's stream
   uint32_t dictBack;  // first chunk: insertions start this far before block 0
   uint32_t low0;      // reference dataZero at the first block (cont only)
+  uint32_t legacy;    // independent blocks (tables reset per block, lookback 0)
+  const Interval* iv;        // assumed shortcut intervals: block b's at iv[b * kMaxIv], ivCount[b] of them
+  const uint32_t* ivCount;
 
-  __device__ __forceinline__ int64_t back(uint32_t b) const
+  __host__ __device__ __forceinline__ int64_t back(uint32_t b) const
   {
+    if (legacy) return 0;
     return (b == 0 && !cont) ? -(int64_t)dictBack : -(int64_t)kTailNoMatch;
   }
-  __device__ __forceinline__ bool dup_block(uint32_t b) const { return b != 0 || cont; }
-  // first position whose entries block b computes (the duplicate excluded)
-  __device__ __forceinline__ int64_t own_lo(uint32_t b) const
+  __host__ __device__ __forceinline__ bool dup_block(uint32_t b) const { return !legacy && (b != 0 || cont); }
+  // first position whose entries block b computes (the duplicate excluded), given its start
+  __host__ __device__ __forceinline__ int64_t own_lo_at(uint32_t b, uint64_t start) const
   {
-    return (int64_t)blocks[b].start + (dup_block(b) ? -(int64_t)kTailNoMatch + 1 : back(b));
+    return (int64_t)start + (dup_block(b) ? -(int64_t)kTailNoMatch + 1 : back(b));
   }
+  __device__ __forceinline__ int64_t own_lo(uint32_t b) const { return own_lo_at(b, blocks[b].start); }
   __device__ __forceinline__ int64_t own_hi(uint32_t b) const { return (int64_t)blocks[b].end - kTailNoMatch; }
   // reference dataZero while block b is compressed (smallz4.h:799-804 keeps the last 64 KiB - 1)
   __device__ __forceinline__ uint64_t low(uint32_t b) const
   {
+    if (legacy) return blocks[b].start;  // only the block's own positions are in the tables
     const int64_t l0 = cont ? (int64_t)low0 : 0;
     if (b == 0) return (uint64_t)l0;
     const int64_t l = (int64_t)blocks[b - 1].end - (int64_t)kWindow;
     return (uint64_t)(l > l0 ? l : l0);
   }
+  // is absolute position pos inside an assumed shortcut interval of block b
+  __device__ __forceinline__ bool skipped(uint32_t b, uint64_t pos) const
+  {
+    const uint32_t n = ivCount[b];
+    const Interval* v = iv + (uint64_t)b * kMaxIv;
+    for (uint32_t k = 0; k < n; k++)
+      if (pos >= v[k].lo && pos < v[k].hi) return true;
+    return false;
+  }
+  // the latest block-relative index <= iw of block b that is == iw (mod 65536) and was inserted: a
+  // shortcut position writes no chain entry, so its slot still holds the one from 65536 indices back
+  __device__ __forceinline__ int64_t inserted_at_or_below(uint32_t b, uint64_t start, int64_t iw) const
+  {
+    const uint32_t n = ivCount[b];
+    if (!n) return iw;
+    const Interval* v = iv + (uint64_t)b * kMaxIv;
+    int64_t pos = (int64_t)start + iw;
+    for (int32_t k = (int32_t)n - 1; k >= 0; k--)  // intervals ascend: a jump only lands lower
+      if (pos >= (int64_t)v[k].lo && pos < (int64_t)v[k].hi)
+        pos -= (((pos - (int64_t)v[k].lo) >> 16) + 1) << 16;
+    return pos - (int64_t)start;
+  }
 };
 
 // the entry slot s holds at insertion step (b, it) of the chunk: written by the latest insertion at or
-// before it with block-relative index == s (mod 65536), or carried from the previous chunk.  `tab`
-// holds every non-duplicate insertion's entry at its staged position.
+// before it with block-relative index == s (mod 65536), or carried from the previous chunk (legacy:
+// nothing before the block, the tables start empty).  `tab` holds every non-duplicate insertion's entry
+// at its staged position.
 __device__ __forceinline__ uint32_t read_slot(const DictPlan& P, const uint16_t* __restrict__ tab,
                                               const uint16_t* __restrict__ carried, uint32_t s, uint32_t b, int64_t it,
                                               uint64_t start, int64_t lo)
 {
-  int64_t iw = it - ((it - (int64_t)s) & (int64_t)kWindow);
+  int64_t iw = P.inserted_at_or_below(b, start, it - ((it - (int64_t)s) & (int64_t)kWindow));
   if (iw >= lo) {  // in the current block (the common case)
     if (iw == -(int64_t)kTailNoMatch && P.dup_block(b)) return 0u;
     return tab[start + iw];
   }
+  if (P.legacy) return 0u;
   for (int32_t bb = (int32_t)b - 1; bb >= 0; bb--) {
     const Block B = P.blocks[bb];
     const int64_t hi = (int64_t)(B.end - B.start) - kTailNoMatch;
-    iw = hi - ((hi - (int64_t)s) & (int64_t)kWindow);
+    iw = P.inserted_at_or_below((uint32_t)bb, B.start, hi - ((hi - (int64_t)s) & (int64_t)kWindow));
     if (iw >= P.back((uint32_t)bb)) {
       if (iw == -(int64_t)kTailNoMatch && P.dup_block((uint32_t)bb)) return 0u;
       return tab[B.start + iw];
@@ -121,72 +158,65 @@ __global__ __launch_bounds__(256) void k_dict_begin(uint32_t* __restrict__ last,
   }
 }
 
-// gate = 1 when a block holds an aligned 32 KiB window of one byte value (a run long enough for the
-// same-letter shortcut contains one)
-__global__ __launch_bounds__(256) void k_dict_detect(const uint8_t* __restrict__ in, uint64_t lo, uint64_t hi,
-                                                     uint32_t* __restrict__ gate)
-{
-  const uint64_t q = ((lo + 32767) & ~32767ull) + (uint64_t)blockIdx.x * 32768u;
-  if (q + 32768 > hi) return;
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + q);
-  const uint32_t first = w[0] & 0xFFu;
-  const uint32_t all = first * 0x01010101u;
-  bool uniform = true;
-  for (uint32_t k = threadIdx.x; k < 8192u; k += 256u) uniform &= w[k] == all;
-  if (__syncthreads_and(uniform) && threadIdx.x == 0) atomicOr(gate, 1u);
-}
-
-__global__ __launch_bounds__(256) void k_dict_keys(const uint8_t* __restrict__ in, uint64_t wlo, uint32_t n,
-                                                   uint64_t* __restrict__ keys)
+// block b's own insertions [ownLo, ownLo + n): (hash << kDictPosBits | index); a shortcut position
+// gets kDictSkipKey and sorts after every hash (never a predecessor, never in the hash table)
+__global__ __launch_bounds__(256) void k_dict_keys(const uint8_t* __restrict__ in, DictPlan P, uint32_t b, uint64_t ownLo,
+                                                   uint32_t n, uint64_t* __restrict__ keys)
 {
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
   if (j >= n) return;
-  keys[j] = ((uint64_t)ref_hash(gload4(in, wlo + j)) << kDictPosBits) | j;
+  const uint64_t p = ownLo + j;
+  const uint32_t h = P.skipped(b, p) ? kDictSkipKey : ref_hash(gload4(in, p));
+  keys[j] = ((uint64_t)h << kDictPosBits) | j;
 }
 
-__global__ __launch_bounds__(256) void k_dict_ph(const uint64_t* __restrict__ keys, uint32_t n, uint64_t wlo,
-                                                 uint64_t ownLo, const uint32_t* __restrict__ last,
-                                                 uint16_t* __restrict__ ph, const uint32_t* __restrict__ gate)
+// previousHash (smallz4.h:648-666): the predecessor in the sorted run of the hash, else the hash
+// table left by the earlier blocks and chunks (legacy: empty before every block)
+__global__ __launch_bounds__(256) void k_dict_ph(const uint64_t* __restrict__ keys, uint32_t n, uint64_t ownLo,
+                                                 const uint32_t* __restrict__ last, uint16_t* __restrict__ ph,
+                                                 uint32_t legacy)
 {
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-  if (j >= n || *gate) return;
+  if (j >= n) return;
   const uint64_t k = keys[j];
-  const uint64_t p = wlo + (k & kDictPosMask);
-  if (p < ownLo) return;  // below the block's own insertions: only a predecessor
   const uint32_t h = (uint32_t)(k >> kDictPosBits);
+  if (h == kDictSkipKey) return;
+  const uint64_t p = ownLo + (k & kDictPosMask);
   uint64_t d = kNone;
   if (j > 0 && (uint32_t)(keys[j - 1] >> kDictPosBits) == h) {
-    d = p - (wlo + (keys[j - 1] & kDictPosMask));
-  } else {
+    d = p - (ownLo + (keys[j - 1] & kDictPosMask));
+  } else if (!legacy) {
     const uint32_t q = last[h];  // the previous chunk's (or an earlier block's) lastHash
     if (q != kDictNoPos && q < p) d = p - q;
   }
   ph[p] = d <= kWindow ? (uint16_t)d : (uint16_t)0;
 }
 
-__global__ __launch_bounds__(256) void k_dict_last(const uint64_t* __restrict__ keys, uint32_t n, uint64_t wlo,
-                                                   uint64_t ownLo, uint32_t* __restrict__ last,
-                                                   const uint32_t* __restrict__ gate)
+__global__ __launch_bounds__(256) void k_dict_last(const uint64_t* __restrict__ keys, uint32_t n, uint64_t ownLo,
+                                                   uint32_t* __restrict__ last)
 {
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-  if (j >= n || *gate) return;
+  if (j >= n) return;
   const uint64_t k = keys[j];
-  const uint64_t p = wlo + (k & kDictPosMask);
   const uint32_t h = (uint32_t)(k >> kDictPosBits);
-  if (p >= ownLo && (j + 1 == n || (uint32_t)(keys[j + 1] >> kDictPosBits) != h)) last[h] = (uint32_t)p;
+  if (h != kDictSkipKey && (j + 1 == n || (uint32_t)(keys[j + 1] >> kDictPosBits) != h))
+    last[h] = (uint32_t)(ownLo + (k & kDictPosMask));
 }
 
 // previousExact (smallz4.h:668-720): from the previousHash candidate, follow the hash chain through
 // snapshot reads while the hash still matches; grid (positions, blocks)
 __global__ __launch_bounds__(256) void k_dict_pe(const uint8_t* __restrict__ in, DictPlan P,
                                                  const uint16_t* __restrict__ ph, const uint16_t* __restrict__ prevH0,
-                                                 uint16_t* __restrict__ pe, const uint32_t* __restrict__ gate)
+                                                 uint16_t* __restrict__ pe)
 {
-  if (*gate) return;
   const uint32_t b = blockIdx.y;
   const int64_t lo = P.own_lo(b), hi = P.own_hi(b);
   const int64_t p = lo + (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (p > hi) return;
+  if (P.skipped(b, (uint64_t)p)) {  // a shortcut position: not inserted, not linked
+    pe[p] = 0;
+    return;
+  }
   const uint64_t start = P.blocks[b].start;
   const int64_t it = p - (int64_t)start, back = P.back(b);
   const uint64_t low = P.low(b);
@@ -230,10 +260,8 @@ __global__ __launch_bounds__(256) void k_dict_pe(const uint8_t* __restrict__ in,
 __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__ in, DictPlan P, uint32_t maxChain,
                                                      const uint16_t* __restrict__ pe, const uint16_t* __restrict__ prevX0,
                                                      uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag,
-                                                     const uint32_t* __restrict__ gate)
+                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
 {
-  if (*gate) return;
   const uint32_t b = blockIdx.y;
   const Block B = P.blocks[b];
   const uint64_t size = B.end - B.start;
@@ -242,7 +270,14 @@ __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__
   const uint64_t pos = B.start + i;
   if (maxChain > (uint32_t)kGreedyMax && i + kTailLiterals >= size) sel[pos] = 0;
   uint32_t bestLen = 0, bestDist = 0;
-  if (i + kTailNoMatch <= size && pe[pos] != 0) {
+  if (P.ivCount[b] && P.skipped(b, pos)) {
+    // same-letter shortcut (smallz4.h:636-641): the interval's distance-1 match, one byte shorter per step
+    const Interval* v = P.iv + (uint64_t)b * kMaxIv;
+    uint32_t k = 0;
+    while (!(pos >= v[k].lo && pos < v[k].hi)) k++;
+    bestLen = (uint32_t)(v[k].La - (pos - v[k].a));
+    bestDist = 1;
+  } else if (i + kTailNoMatch <= size && pe[pos] != 0) {
     const int64_t back = P.back(b);
     const uint64_t stop = B.end - kTailLiterals;
     bestLen = 1;
@@ -274,8 +309,8 @@ __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__
   mdist[pos] = (uint16_t)bestDist;
   // optimal levels search every linked position: the parse's range-minimum flag is set here
   if (maxChain > (uint32_t)kLazyMax) {
-    const bool rmq = bestLen >= kDictRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
-    if (__ballot(rmq) && lane_id() == 0) atomicOr(longFlag + b, 1u);
+    const bool rmq = bestLen >= kRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
+    if (__ballot(rmq) && lane_id() == 0) atomicOr(longFlag + b, kFlagRmq);
   }
 }
 
@@ -372,10 +407,9 @@ __device__ __forceinline__ void lz_setbit(uint32_t* m, uint32_t i)
 __global__ __launch_bounds__(64 * 4) void k_dict_lz_walk(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
                                                          uint32_t nwalk, const uint32_t* __restrict__ mlen,
                                                          const uint16_t* __restrict__ pe, uint32_t* __restrict__ masks,
-                                                         uint4* __restrict__ state, const uint32_t* __restrict__ gate)
+                                                         uint4* __restrict__ state)
 {
   __shared__ uint32_t bits[4][2 * kLzWords];
-  if (*gate) return;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t idx = blockIdx.x * 4 + wave;
   if (idx >= nwalk) return;
@@ -409,10 +443,9 @@ __global__ __launch_bounds__(64 * 4) void k_dict_lz_walk(const Block* __restrict
 
 __global__ __launch_bounds__(64) void k_dict_lz_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ mlen,
                                                     const uint16_t* __restrict__ pe, uint32_t* __restrict__ masks,
-                                                    uint4* __restrict__ state, const uint32_t* __restrict__ gate)
+                                                    uint4* __restrict__ state)
 {
   __shared__ uint32_t fresh[kLzWords], rep[kLzWords];
-  if (*gate) return;
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = (uint32_t)(B.end - B.start);
@@ -471,10 +504,8 @@ __global__ __launch_bounds__(64) void k_dict_lz_fix(const Block* __restrict__ bl
 __global__ __launch_bounds__(64 * 4) void k_dict_lz_clear(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
                                                           uint32_t nwalk, uint32_t* __restrict__ mlen,
                                                           uint16_t* __restrict__ mdist, const uint16_t* __restrict__ pe,
-                                                          const uint32_t* __restrict__ masks, uint32_t* __restrict__ longFlag,
-                                                          const uint32_t* __restrict__ gate)
+                                                          const uint32_t* __restrict__ masks, uint32_t* __restrict__ longFlag)
 {
-  if (*gate) return;
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t idx = blockIdx.x * 4 + wave;
   if (idx >= nwalk) return;
@@ -500,18 +531,17 @@ __global__ __launch_bounds__(64 * 4) void k_dict_lz_clear(const Block* __restric
       }
     } else {
       const uint32_t L = mlen[p];
-      if (L >= kDictRmqLen) rmq |= !(mdist[p] == 1u && L >= kSameLetter);
+      if (L >= kRmqLen) rmq |= !(mdist[p] == 1u && L >= kSameLetter);
     }
   }
-  if (__ballot(rmq) && lane == 0) atomicOr(longFlag + ws.x, 1u);
+  if (__ballot(rmq) && lane == 0) atomicOr(longFlag + ws.x, kFlagRmq);
 }
 
 // the chain tables after the chunk's last insertion, in place (slot s reads only its own carried value)
 __global__ __launch_bounds__(256) void k_dict_carry(DictPlan P, const uint16_t* __restrict__ ph,
                                                     const uint16_t* __restrict__ pe, uint16_t* __restrict__ prevH,
-                                                    uint16_t* __restrict__ prevX, const uint32_t* __restrict__ gate)
+                                                    uint16_t* __restrict__ prevX)
 {
-  if (*gate) return;
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
   if (s >= 65536u) return;
   const uint32_t b = P.nb - 1;
@@ -524,71 +554,155 @@ __global__ __launch_bounds__(256) void k_dict_carry(DictPlan P, const uint16_t* 
   prevX[s] = x;
 }
 
+
+// ---- the shortcut intervals the results imply (smallz4.h:631-643) --------------------------------
+// bit a of a block: block-relative a is searched (not assumed skipped) and found a distance-1 match
+// longer than MaxSameLetter, so the reference's loop would skip a + 1 .. a + La - MaxSameLetter.
+// Positions assumed skipped have no search result, so they start nothing (the next round searches them).
+__global__ __launch_bounds__(256) void k_dict_sc_bits(DictPlan P, const uint32_t* __restrict__ mlen,
+                                                      const uint16_t* __restrict__ mdist, uint64_t* __restrict__ bits,
+                                                      uint64_t wordsPerBlock)
+{
+  const uint32_t b = blockIdx.y;
+  const Block B = P.blocks[b];
+  const uint64_t n = B.end - B.start;
+  const uint64_t a = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (a >= ((n + 63) & ~63ull)) return;
+  const uint64_t pos = B.start + a;
+  // a + 1 must be a position of the loop: a + 1 + 12 <= n
+  const bool q = a + 1 + kTailNoMatch <= n && mdist[pos] == 1u && mlen[pos] > kSameLetter && !P.skipped(b, pos);
+  const uint64_t m = __ballot(q);
+  if (lane_id() == 0) bits[(uint64_t)b * wordsPerBlock + (a >> 6)] = m;
+}
+
+// one wavefront per block: the intervals in the order the reference's loop meets them (a start inside an
+// interval already taken is not a start), compared with the assumed ones; a difference replaces them
+// and raises kStPrepRound
+__global__ __launch_bounds__(64) void k_dict_sc(const Block* __restrict__ blocks, const uint64_t* __restrict__ bits,
+                                                uint64_t wordsPerBlock, const uint32_t* __restrict__ mlen,
+                                                Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount,
+                                                int* __restrict__ status)
+{
+  __shared__ Interval ys[kMaxIv];
+  const uint32_t b = blockIdx.x, lane = threadIdx.x;
+  const Block B = blocks[b];
+  const uint64_t n = B.end - B.start;
+  const uint64_t* w = bits + (uint64_t)b * wordsPerBlock;
+  const uint64_t words = (n + 63) / 64;
+  uint32_t ny = 0;
+  bool overflow = false;
+  uint64_t from = 0;  // block-relative: the next position that may start an interval
+  for (uint64_t w0 = 0; w0 < words; w0 += 64) {
+    uint64_t mine = w0 + lane < words ? w[w0 + lane] : 0ull;
+    while (true) {
+      // clear the bits below `from`
+      const uint64_t base = (w0 + lane) * 64;
+      if (base + 64 <= from) mine = 0;
+      else if (base < from) mine &= ~0ull << (from - base);
+      const uint64_t any = __ballot(mine != 0);
+      if (!any) break;
+      const uint32_t l = (uint32_t)__builtin_ctzll(any);
+      const uint64_t word = ((uint64_t)rdlane((uint32_t)(mine >> 32), l) << 32) | rdlane((uint32_t)mine, l);
+      const uint64_t a = (w0 + l) * 64 + (uint64_t)__builtin_ctzll(word);
+      const uint32_t La = mlen[B.start + a];
+      if (ny < kMaxIv) {
+        if (lane == 0) {
+          Interval x;
+          x.a = B.start + a;
+          x.La = La;
+          x.lo = x.a + 1;
+          x.hi = x.lo + (La - kSameLetter);
+          ys[ny] = x;
+        }
+        ny++;
+      } else {
+        overflow = true;
+      }
+      from = a + 1 + (La - kSameLetter);
+    }
+  }
+  __syncthreads();
+  if (overflow) {
+    if (lane == 0) atomicOr(status, kStInvariant);
+    return;
+  }
+  Interval* xs = ivAll + (uint64_t)b * kMaxIv;
+  const uint32_t nx = ivCount[b];
+  bool same = nx == ny;
+  if (same) {
+    bool diff = false;
+    for (uint32_t k = lane; k < ny; k += 64)
+      diff |= xs[k].lo != ys[k].lo || xs[k].hi != ys[k].hi || xs[k].La != ys[k].La;
+    same = __ballot(diff) == 0;
+  }
+  if (same) return;
+  for (uint32_t k = lane; k < ny; k += 64) xs[k] = ys[k];
+  if (lane == 0) {
+    ivCount[b] = ny;
+    atomicOr(status, kStPrepRound);
+  }
+}
+
 uint64_t dict_lz_mask_bytes_per_walk() { return 2 * kLzWords * 4; }
 
-uint64_t dict_sort_keys_max() { return kBlockMaxDict + kWindow + 64; }
+uint64_t dict_sort_keys_max() { return kBlockMaxLegacy + 64; }
 
 uint64_t dict_sort_temp_bytes()
 {
   size_t bytes = 0;
-  rocprim::radix_sort_keys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)dict_sort_keys_max(), 0,
-                           kHashBits + kDictPosBits, (hipStream_t)0);
+  if (rocprim::radix_sort_keys(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr, (size_t)dict_sort_keys_max(), 0,
+                               kDictSortBits, (hipStream_t)0) != hipSuccess)
+    return 0;
   return bytes;
 }
 
-int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* hBlocks, uint32_t nb, uint32_t maxChain,
-                         uint32_t dictBack, uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH,
-                         uint16_t* prevX, uint16_t* ph, uint16_t* pe, uint64_t* keysA, uint64_t* keysB, void* temp,
-                         uint64_t tempBytes, uint32_t* gate, uint32_t* mlen, uint16_t* mdist, uint32_t* sel,
-                         uint32_t* longFlag, const uint2* walkSegs, uint32_t nwalk, uint32_t* lzMasks, uint4* lzState,
-                         hipStream_t s)
+int launch_dict_parallel(const DictArgs& A, hipStream_t s)
 {
+  const uint32_t nb = A.nb;
   if (!nb) return 0;
-  if (hipMemsetAsync(gate, 0, 4, s)) return -1;
-  hipLaunchKernelGGL(k_dict_begin, dim3((1u << kHashBits) / 256), dim3(256), 0, s, last, prevH, prevX, cont, shift);
-  const uint64_t lo = hBlocks[0].start, hi = hBlocks[nb - 1].end;
-  const uint64_t wins = (hi - lo) / 32768 + 1;
-  hipLaunchKernelGGL(k_dict_detect, dim3((uint32_t)wins), dim3(256), 0, s, in, lo, hi, gate);
-  // the serial replay runs only for a gated chunk (its tables were prepared by k_dict_begin)
-  launch_dict_gated(in, dBlocks, nb, maxChain, dictBack, cont, shift, low0, last, prevH, prevX, mlen, mdist, sel, longFlag,
-                    gate, s);
-  DictPlan P{dBlocks, nb, cont, dictBack, low0};
-  // previousHash: per block, a sort of its own insertions and the 64 KiB below them
-  int64_t p0 = 0;
+  DictPlan P{A.dBlocks, nb, A.cont, A.dictBack, A.low0, A.legacy ? 1u : 0u, A.iv, A.ivCount};
+  if (!A.legacy)
+    hipLaunchKernelGGL(k_dict_begin, dim3((1u << kHashBits) / 256), dim3(256), 0, s, A.last, A.prevH, A.prevX, A.cont,
+                       A.shift);
+  // previousHash: per block, a sort of its own insertions (earlier ones through the hash table)
   uint32_t maxOwn = 0, maxSize = 0;
   for (uint32_t b = 0; b < nb; b++) {
-    const Block& B = hBlocks[b];
-    const bool dupB = b != 0 || cont;
-    const int64_t back = (b == 0 && !cont) ? -(int64_t)dictBack : -(int64_t)kTailNoMatch;
-    const int64_t ownLo = (int64_t)B.start + (dupB ? -(int64_t)kTailNoMatch + 1 : back);
+    const Block& B = A.hBlocks[b];
+    const int64_t ownLo = P.own_lo_at(b, B.start);
     const int64_t ownHi = (int64_t)B.end - kTailNoMatch;
-    if (b == 0) p0 = ownLo;
     maxSize = std::max<uint32_t>(maxSize, (uint32_t)(B.end - B.start));
     if (ownHi < ownLo) continue;
-    maxOwn = std::max<uint32_t>(maxOwn, (uint32_t)(ownHi - ownLo + 1));
-    const int64_t wlo = std::max<int64_t>(p0, ownLo - (int64_t)kWindow);
-    const uint32_t n = (uint32_t)(ownHi - wlo + 1);
+    const uint32_t n = (uint32_t)(ownHi - ownLo + 1);
+    maxOwn = std::max<uint32_t>(maxOwn, n);
     if ((uint64_t)n > dict_sort_keys_max()) return -1;
     const uint32_t g = (n + 255) / 256;
-    hipLaunchKernelGGL(k_dict_keys, dim3(g), dim3(256), 0, s, in, (uint64_t)wlo, n, keysA);
-    size_t tb = tempBytes;
-    if (rocprim::radix_sort_keys(temp, tb, keysA, keysB, (size_t)n, 0, kHashBits + kDictPosBits, s)) return -1;
-    hipLaunchKernelGGL(k_dict_ph, dim3(g), dim3(256), 0, s, keysB, n, (uint64_t)wlo, (uint64_t)ownLo, last, ph, gate);
-    hipLaunchKernelGGL(k_dict_last, dim3(g), dim3(256), 0, s, keysB, n, (uint64_t)wlo, (uint64_t)ownLo, last, gate);
+    hipLaunchKernelGGL(k_dict_keys, dim3(g), dim3(256), 0, s, A.in, P, b, (uint64_t)ownLo, n, A.keysA);
+    size_t tb = A.tempBytes;
+    if (rocprim::radix_sort_keys(A.temp, tb, A.keysA, A.keysB, (size_t)n, 0, kDictSortBits, s)) return -1;
+    hipLaunchKernelGGL(k_dict_ph, dim3(g), dim3(256), 0, s, A.keysB, n, (uint64_t)ownLo, A.last, A.ph,
+                       A.legacy ? 1u : 0u);
+    if (!A.legacy) hipLaunchKernelGGL(k_dict_last, dim3(g), dim3(256), 0, s, A.keysB, n, (uint64_t)ownLo, A.last);
   }
   if (maxOwn)
-    hipLaunchKernelGGL(k_dict_pe, dim3((maxOwn + 255) / 256, nb), dim3(256), 0, s, in, P, ph, prevH, pe, gate);
-  hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 255) / 256, nb), dim3(256), 0, s, in, P, maxChain, pe, prevX, mlen, mdist,
-                     sel, longFlag, gate);
-  if (maxChain <= (uint32_t)kLazyMax && nwalk) {
-    hipLaunchKernelGGL(k_dict_lz_walk, dim3((nwalk + 3) / 4), dim3(256), 0, s, dBlocks, walkSegs, nwalk, mlen, pe, lzMasks,
-                       lzState, gate);
-    hipLaunchKernelGGL(k_dict_lz_fix, dim3(nb), dim3(64), 0, s, dBlocks, mlen, pe, lzMasks, lzState, gate);
-    hipLaunchKernelGGL(k_dict_lz_clear, dim3((nwalk + 3) / 4), dim3(256), 0, s, dBlocks, walkSegs, nwalk, mlen, mdist, pe,
-                       lzMasks, longFlag, gate);
+    hipLaunchKernelGGL(k_dict_pe, dim3((maxOwn + 255) / 256, nb), dim3(256), 0, s, A.in, P, A.ph, A.prevH, A.pe);
+  hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 255) / 256, nb), dim3(256), 0, s, A.in, P, A.maxChain, A.pe, A.prevX,
+                     A.mlen, A.mdist, A.sel, A.longFlag);
+  if (A.maxChain <= (uint32_t)kLazyMax && A.nwalk) {
+    hipLaunchKernelGGL(k_dict_lz_walk, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
+                       A.pe, A.lzMasks, A.lzState);
+    hipLaunchKernelGGL(k_dict_lz_fix, dim3(nb), dim3(64), 0, s, A.dBlocks, A.mlen, A.pe, A.lzMasks, A.lzState);
+    hipLaunchKernelGGL(k_dict_lz_clear, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
+                       A.mdist, A.pe, A.lzMasks, A.longFlag);
   }
-  hipLaunchKernelGGL(k_dict_carry, dim3(65536 / 256), dim3(256), 0, s, P, ph, pe, prevH, prevX, gate);
+  if (!A.legacy) hipLaunchKernelGGL(k_dict_carry, dim3(65536 / 256), dim3(256), 0, s, P, A.ph, A.pe, A.prevH, A.prevX);
+  // the intervals these results imply (the host runs the chunk again if they differ)
+  const uint64_t wpb = (maxSize + 63) / 64;
+  hipLaunchKernelGGL(k_dict_sc_bits, dim3((uint32_t)((wpb * 64 + 255) / 256), nb), dim3(256), 0, s, P, A.mlen, A.mdist,
+                     A.scBits, wpb);
+  hipLaunchKernelGGL(k_dict_sc, dim3(nb), dim3(64), 0, s, A.dBlocks, A.scBits, wpb, A.mlen, A.iv, A.ivCount, A.status);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+uint64_t dict_sc_bits_bytes(uint32_t nb, uint64_t maxBlock) { return (uint64_t)nb * ((maxBlock + 63) / 64) * 8 + 64; }
 
 }  // namespace sz4

@@ -31,8 +31,8 @@ namespace {
 
 constexpr uint64_t kPad = 64;                 // bytes of slack after every staged input
 constexpr uint64_t kSegTargets = 65536;       // target positions per segment
-constexpr uint64_t kBlockMax = 4ull << 20;    // MaxBlockSize (smallz4.h:124)
-constexpr uint64_t kBlockMaxLegacy = 8ull << 20;
+constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
+constexpr uint32_t kDictMaxRounds = 4 * kMaxIv;  // dictionary rounds before the in-order replay takes the chunk
 
 uint64_t token_capacity(uint64_t n) { return n / 2 + 4; }
 
@@ -132,7 +132,9 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
-  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictGate, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
+  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
+  uint32_t dictRounds = 0;  // rounds the last dictionary chunk took (~0u: it fell back to the in-order replay)
+  uint64_t dictTempBytes = 0;  // rocPRIM radix sort scratch for dictKeys (queried on first use)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
   DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
@@ -180,7 +182,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictGate, &dictLz,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictLz,
             &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
             &unOut, &unSeq};
   }
@@ -356,31 +358,99 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
   if (c->dictBack < 0) launch_runs(in, dB, nb, dIv, dIvN, s);
   mark(c, 1, s);
   if (c->dictBack >= 0 && maxChain > 0) {
-    // dictionary mode: the reference's sequential match loop (k_dict_matches), then the usual parse
+    // dictionary mode (modern and legacy frames): the data-parallel match finder of sz4_dict.hip, in
+    // rounds until its assumed same-letter shortcut intervals are the ones its results imply; then the
+    // usual parse
     if ((e = c->dictLast.reserve(sizeof(uint32_t) << 20)) || (e = c->dictPrevH.reserve(2 * 65536)) ||
         (e = c->dictPrevX.reserve(2 * 65536)))
       return c->fail(SZ4_E_NOMEM, "dictionary tables", e);
-    if (c->dictLegacy || c->dictSerial) {
-      // legacy frames reset the tables every block: the reference's loop replayed in order
+    auto serial = [&]() {
       launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
                   c->dictPrevH.as<uint16_t>(), c->dictPrevX.as<uint16_t>(), c->dictCont, c->dictShift, c->dictLow0,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s);
+    };
+    if (c->dictSerial) {
+      serial();  // A/B and tests: the reference's loop replayed in order by one wavefront
     } else {
       const uint64_t staged = c->hBlocks.back().end + 64;
-      static const uint64_t tempBytes = dict_sort_temp_bytes();
+      uint64_t maxBlock = 0;
+      for (const Block& B : c->hBlocks) maxBlock = std::max<uint64_t>(maxBlock, B.end - B.start);
+      // rocPRIM's scratch size, queried once per context on its own device (0: the query failed)
+      if (!c->dictTempBytes && !(c->dictTempBytes = dict_sort_temp_bytes()))
+        return c->fail(SZ4_E_DEVICE, "dictionary sort: scratch size query");
+      const uint64_t lastBytes = sizeof(uint32_t) << kHashBits, slotBytes = 2 * 65536;
       if ((e = c->dictPH.reserve(staged * 2)) || (e = c->dictPE.reserve(staged * 2)) ||
-          (e = c->dictKeys.reserve(2 * dict_sort_keys_max() * 8)) || (e = c->dictTemp.reserve(tempBytes + 64)) ||
-          (e = c->dictGate.reserve(64)) ||
+          (e = c->dictKeys.reserve(2 * dict_sort_keys_max() * 8)) || (e = c->dictTemp.reserve(c->dictTempBytes + 64)) ||
+          (e = c->dictSc.reserve(dict_sc_bits_bytes(nb, maxBlock))) ||
+          (e = c->dictSnap.reserve(lastBytes + 2 * slotBytes)) ||
           (e = c->dictLz.reserve(c->hWalk.size() * dict_lz_mask_bytes_per_walk() + 64)))
         return c->fail(SZ4_E_NOMEM, "dictionary scratch", e);
-      if (launch_dict_parallel(in, dB, c->hBlocks.data(), nb, maxChain, (uint32_t)c->dictBack, c->dictCont, c->dictShift,
-                               c->dictLow0, c->dictLast.as<uint32_t>(), c->dictPrevH.as<uint16_t>(),
-                               c->dictPrevX.as<uint16_t>(), c->dictPH.as<uint16_t>(), c->dictPE.as<uint16_t>(),
-                               c->dictKeys.as<uint64_t>(), c->dictKeys.as<uint64_t>() + dict_sort_keys_max(), c->dictTemp.p,
-                               tempBytes, c->dictGate.as<uint32_t>(), c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(),
-                               c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), c->walkSegs.as<uint2>(),
-                               (uint32_t)c->hWalk.size(), c->dictLz.as<uint32_t>(), c->walkState.as<uint4>(), s))
-        return c->fail(SZ4_E_DEVICE, "dictionary kernels");
+      // the carried tables as this chunk found them: a round that finds other shortcut intervals starts
+      // again from here (legacy frames carry nothing: every block starts from empty tables)
+      uint8_t* snap = c->dictSnap.as<uint8_t>();
+      auto tables = [&](bool save) -> hipError_t {
+        hipError_t r;
+        uint8_t* t[3] = {c->dictLast.as<uint8_t>(), c->dictPrevH.as<uint8_t>(), c->dictPrevX.as<uint8_t>()};
+        const uint64_t off[3] = {0, lastBytes, lastBytes + slotBytes}, len[3] = {lastBytes, slotBytes, slotBytes};
+        for (int k = 0; k < 3; k++)
+          if ((r = hipMemcpyAsync(save ? snap + off[k] : t[k], save ? t[k] : snap + off[k], len[k],
+                                  hipMemcpyDeviceToDevice, s)))
+            return r;
+        return hipSuccess;
+      };
+      if ((!c->dictLegacy && (e = tables(true))) || (e = hipMemsetAsync(dIvN, 0, nb * 4, s)))
+        return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
+      DictArgs A{};
+      A.in = in;
+      A.dBlocks = dB;
+      A.hBlocks = c->hBlocks.data();
+      A.nb = nb;
+      A.maxChain = maxChain;
+      A.dictBack = (uint32_t)c->dictBack;
+      A.cont = c->dictCont;
+      A.shift = c->dictShift;
+      A.low0 = c->dictLow0;
+      A.legacy = c->dictLegacy;
+      A.iv = dIv;
+      A.ivCount = dIvN;
+      A.last = c->dictLast.as<uint32_t>();
+      A.prevH = c->dictPrevH.as<uint16_t>();
+      A.prevX = c->dictPrevX.as<uint16_t>();
+      A.ph = c->dictPH.as<uint16_t>();
+      A.pe = c->dictPE.as<uint16_t>();
+      A.keysA = c->dictKeys.as<uint64_t>();
+      A.keysB = c->dictKeys.as<uint64_t>() + dict_sort_keys_max();
+      A.temp = c->dictTemp.p;
+      A.tempBytes = c->dictTempBytes;
+      A.mlen = c->mlen.as<uint32_t>();
+      A.mdist = c->mdist.as<uint16_t>();
+      A.sel = c->sel.as<uint32_t>();
+      A.longFlag = c->longFlag.as<uint32_t>();
+      A.walkSegs = c->walkSegs.as<uint2>();
+      A.nwalk = (uint32_t)c->hWalk.size();
+      A.lzMasks = c->dictLz.as<uint32_t>();
+      A.lzState = c->walkState.as<uint4>();
+      A.scBits = c->dictSc.as<uint64_t>();
+      A.status = c->status.as<int>();
+      for (uint32_t round = 0;; round++) {
+        if (round > 0 && ((!c->dictLegacy && (e = tables(false))) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s))))
+          return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
+        if (launch_dict_parallel(A, s)) return c->fail(SZ4_E_DEVICE, "dictionary kernels");
+        int st = 0;
+        if ((e = hipMemcpyAsync(&st, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+          return c->fail(SZ4_E_DEVICE, "dictionary rounds", e);
+        c->dictRounds = round + 1;
+        if (!(st & (kStPrepRound | kStInvariant))) break;
+        if ((e = hipMemsetAsync(c->status.p, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "dictionary rounds", e);
+        // every round settles a longer prefix, so this is a safety net, not a path: the in-order replay
+        if ((st & kStInvariant) || round + 1 >= kDictMaxRounds) {
+          if ((!c->dictLegacy && (e = tables(false))) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
+            return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
+          serial();
+          c->dictRounds = ~0u;
+          break;
+        }
+      }
     }
     mark(c, 2, s);
     mark(c, 3, s);
@@ -1335,6 +1405,8 @@ uint64_t sz4_device_bytes(sz4_ctx* c)
   for (const DevBuf* b : c->all_buffers()) t += b->cap;
   return t;
 }
+
+uint32_t sz4_dict_rounds(sz4_ctx* c) { return c ? c->dictRounds : 0u; }
 
 const char* sz4_last_error(sz4_ctx* c) { return c ? c->err.c_str() : "no context"; }
 

@@ -18,6 +18,10 @@ constexpr int kLazyMax = 6;              // ShortChainsLazy
 constexpr uint32_t kHashMul = 48271;     // getHash32 multiplier
 constexpr int kHashBits = 20;
 constexpr uint64_t kNone = ~0ull;
+// the parse's per-block flags (longFlag), set by every match finder (sz4_kernels.hip, sz4_dict.hip)
+constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima
+constexpr uint32_t kFlagRmq = 1;   // the block has matches of kRmqLen+ (other than same-letter runs)
+constexpr uint32_t kFlagRun = 2;   // a distance-1 match longer than MaxSameLetter (bounded chains)
 constexpr int kStages = 6;  // runs, sort, find (sorted pass), find (long pass), parse, assemble
 
 // device status word bits (one int per pipeline run)
@@ -113,24 +117,41 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
 void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack, int legacy,
                  uint32_t* last, uint16_t* prevH, uint16_t* prevX, uint32_t cont, uint32_t shift, uint32_t low0,
                  uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, hipStream_t s);
-// the same replay behind a device gate: it runs only if *gate != 0 (k_dict_detect found a run long
-// enough for the same-letter shortcut), with the tables already prepared by k_dict_begin
-void launch_dict_gated(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack,
-                       uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH, uint16_t* prevX,
-                       uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, const uint32_t* gate,
-                       hipStream_t s);
-// dictionary mode on the whole GPU (sz4_dict.hip), non-legacy frames: hBlocks is the host copy of the
-// plan, walkSegs the token walk's sub-segments; ph / pe: one u16 per staged position; keysA / keysB: dict_sort_keys_max() u64 each; temp:
-// dict_sort_temp_bytes(); gate: one u32.  Returns 0, or -1 on a launch failure
-constexpr uint64_t kBlockMaxDict = 4ull << 20;  // MaxBlockSize (smallz4.h:124)
+// dictionary mode on the whole GPU (sz4_dict.hip), modern and legacy frames: hBlocks is the host copy of
+// the plan, walkSegs the token walk's sub-segments; ph / pe: one u16 per staged position; keysA / keysB:
+// dict_sort_keys_max() u64 each; temp: dict_sort_temp_bytes(); scBits: dict_sc_bits_bytes().  iv /
+// ivCount: the assumed same-letter shortcut intervals per block (kMaxIv each); the launch replaces them
+// with the ones its results imply and raises kStPrepRound in *status when they differ (then the chunk
+// is run again from its saved tables).  Returns 0, or -1 on a launch failure
+constexpr uint64_t kBlockMaxDict = 4ull << 20;     // MaxBlockSize (smallz4.h:124)
+constexpr uint64_t kBlockMaxLegacy = 8ull << 20;   // MaxBlockSizeLegacy (smallz4.h:125)
+struct DictArgs {
+  const uint8_t* in;
+  const Block* dBlocks;
+  const Block* hBlocks;
+  uint32_t nb, maxChain, dictBack, cont, shift, low0;
+  int legacy;
+  Interval* iv;
+  uint32_t* ivCount;
+  uint32_t* last;
+  uint16_t *prevH, *prevX, *ph, *pe;
+  uint64_t *keysA, *keysB;
+  void* temp;
+  uint64_t tempBytes;
+  uint32_t* mlen;
+  uint16_t* mdist;
+  uint32_t *sel, *longFlag;
+  const uint2* walkSegs;
+  uint32_t nwalk;
+  uint32_t* lzMasks;
+  uint4* lzState;
+  uint64_t* scBits;
+  int* status;
+};
 uint64_t dict_sort_keys_max();
-uint64_t dict_sort_temp_bytes();
-int launch_dict_parallel(const uint8_t* in, const Block* dBlocks, const Block* hBlocks, uint32_t nb, uint32_t maxChain,
-                         uint32_t dictBack, uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH,
-                         uint16_t* prevX, uint16_t* ph, uint16_t* pe, uint64_t* keysA, uint64_t* keysB, void* temp,
-                         uint64_t tempBytes, uint32_t* gate, uint32_t* mlen, uint16_t* mdist, uint32_t* sel,
-                         uint32_t* longFlag, const uint2* walkSegs, uint32_t nwalk, uint32_t* lzMasks, uint4* lzState,
-                         hipStream_t s);
+uint64_t dict_sort_temp_bytes();  // rocPRIM's scratch for dict_sort_keys_max() keys; 0 if the query failed
+uint64_t dict_sc_bits_bytes(uint32_t nb, uint64_t maxBlock);
+int launch_dict_parallel(const DictArgs& a, hipStream_t s);
 // greedy/lazy levels: dict_lz_mask_bytes_per_walk() bytes per token-walk sub-segment (lzMasks), one
 // uint4 per sub-segment (lzState)
 uint64_t dict_lz_mask_bytes_per_walk();

@@ -731,9 +731,6 @@ constexpr uint32_t kBigRunL = SZ4_BIG_RUN_L;  // ... in blocks above 64 KiB (k_f
 constexpr uint32_t kLpfMin = SZ4_LPF_MIN;     // ... and for an LPF target (below)
 constexpr uint32_t kLpfProbe = 8;
 __device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
-constexpr uint32_t kRmqLen = 274;  // match lengths from here on use the parse's range minima (longFlag)
-constexpr uint32_t kFlagRmq = 1;   // longFlag: the block has matches of kRmqLen+ (other than same-letter runs)
-constexpr uint32_t kFlagRun = 2;   // longFlag: a distance-1 match longer than MaxSameLetter (bounded chains)
 // k_find_sorted's results leave in text order, tiles of kOutTile positions staged in LDS
 constexpr uint32_t kOutTileBits = 14;
 constexpr uint32_t kOutTile = 1u << kOutTileBits;    // 64 KiB of LDS as u32
@@ -3491,13 +3488,9 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
                                                      uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
                                                      uint16_t* __restrict__ prevXg, uint32_t cont, uint32_t shift,
                                                      uint32_t low0, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag,
-                                                     const uint32_t* __restrict__ gate)
+                                                     uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
 {
   __shared__ uint16_t prevX[65536];
-  // gate: the data-parallel path (sz4_dict.hip) takes the chunk unless k_dict_detect set it, and its
-  // k_dict_begin has already prepared the carried tables
-  if (gate && *gate == 0u) return;
   const uint32_t lane = threadIdx.x;
   auto reset = [&]() {
     for (uint32_t j = lane; j < 65536; j += 64) {
@@ -3506,9 +3499,7 @@ __global__ __launch_bounds__(64) void k_dict_matches(const uint8_t* __restrict__
     }
     for (uint32_t j = lane; j < (1u << kHashBits); j += 64) last[j] = kNoPos;
   };
-  if (gate) {
-    for (uint32_t j = lane; j < 65536; j += 64) prevX[j] = prevXg[j];
-  } else if (!cont) {
+  if (!cont) {
     reset();
   } else {
     // the previous chunk's tables: chain slots are absolute positions mod 65536, unchanged by a shift
@@ -3641,17 +3632,7 @@ void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint3
 {
   if (nblocks)
     hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, legacy, last, prevH,
-                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag, (const uint32_t*)nullptr);
-}
-
-void launch_dict_gated(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint32_t maxChain, uint32_t dictBack,
-                       uint32_t cont, uint32_t shift, uint32_t low0, uint32_t* last, uint16_t* prevH, uint16_t* prevX,
-                       uint32_t* mlen, uint16_t* mdist, uint32_t* sel, uint32_t* longFlag, const uint32_t* gate,
-                       hipStream_t s)
-{
-  if (nblocks)
-    hipLaunchKernelGGL(k_dict_matches, dim3(1), dim3(64), 0, s, in, blocks, nblocks, maxChain, dictBack, 0, last, prevH,
-                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag, gate);
+                       prevX, cont, shift, low0, mlen, mdist, sel, longFlag);
 }
 
 // Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut

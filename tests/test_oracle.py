@@ -188,3 +188,19 @@ def test_reference_legacy_level0_loses_data():
     assert frame == bytes.fromhex("02214c1800000000")
     out = subprocess.run([pyoracle.REF_CAT], input=frame, capture_output=True, check=True).stdout
     assert out == b"" == pyoracle.oz_unlz4(frame)
+
+
+def test_oracle_matches_stream_fixtures():
+    """tests/golden/streams.json (whole-stream fixtures of the reference, checked on the GPU by
+    test_stream.py): the C restatement reproduces the cases the reference itself finishes in about a
+    second (dictionary runs at -6 / -3, legacy frames with a dictionary at -3)."""
+    import json
+    import inputs
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "streams.json")) as f:
+        cases = [c for c in json.load(f)["cases"] if c["ref_seconds"] <= 1.5]
+    assert len(cases) >= 3
+    for c in cases:
+        data = inputs.make(c["input"])
+        dic = inputs.make(c["dictionary"]) if c["dictionary"] else b""
+        out = pyoracle.oz_lz4(data, c["max_chain"], dic, c["legacy"])
+        assert len(out) == c["frame_len"] and inputs.sha(out) == c["frame_sha256"], c["name"]

@@ -108,14 +108,59 @@ def test_chunked_dictionary_multi_block_chunks(compressor, chain):
 
 
 @pytest.mark.parametrize("chain", [3, 6])
-def test_dictionary_long_run_gate(chunked, chain):
-    """A run of one byte value long enough for the same-letter shortcut (> 65 300 bytes) sends its chunk
-    to the in-order replay (k_dict_detect's gate); the next chunk continues on the data-parallel path
-    from the tables the replay left.  Short runs (< 32 KiB windows) stay on the parallel path."""
+def test_dictionary_long_run_rounds(chunked, chain):
+    """A run of one byte value long enough for the same-letter shortcut (> 65 300 bytes) in dictionary
+    mode: the data-parallel finder runs its chunk again with the shortcut intervals its first results
+    imply (sz4_dict.hip), and the next chunk continues from the tables that round left.  No in-order
+    replay."""
     data = (synth.enwik8_like(M - 120000, seed=70) + b"a" * 70000 + synth.enwik8_like(50000, seed=71) +
             bytes(30000) + synth.enwik8_like(M // 2, seed=72))
     dictionary = b"a" * 1000 + synth.enwik8_like(9000, seed=73)
     assert chunked.lz4(data, chain, dictionary) == pyoracle.oz_lz4(data, chain, dictionary)
+    assert chunked.dict_rounds() != 0xFFFFFFFF
+
+
+def _streams_golden():
+    with open(os.path.join(ROOT, "tests", "golden", "streams.json")) as f:
+        return {c["name"]: c for c in json.load(f)["cases"]}
+
+
+def _stream_case(name):
+    case = _streams_golden()[name]
+    data = inputs.make(case["input"])
+    assert inputs.sha(data) == case["input_sha256"]
+    dic = inputs.make(case["dictionary"]) if case["dictionary"] else b""
+    assert inputs.sha(dic) == case["dictionary_sha256"]
+    return case, data, dic
+
+
+@pytest.mark.parametrize("name", sorted(_streams_golden()))
+def test_dictionary_stream_fixtures(compressor, name):
+    """The reference's own frames for dictionary streams it is too slow to redo inside a test
+    (tests/golden/streams.json, made by make_streams_golden.py: a long run makes its chain walk
+    quadratic): runs long enough for the same-letter shortcut -- in the middle of 8 MB, across blocks,
+    at a 16 KiB-unaligned offset, in configs[4]-shaped zeros/urandom data -- and legacy frames with a
+    dictionary, at -9, -6 and -3.  All on the data-parallel path (no in-order replay)."""
+    case, data, dic = _stream_case(name)
+    out = compressor.lz4(data, case["max_chain"], dic, case["legacy"])
+    assert len(out) == case["frame_len"] and inputs.sha(out) == case["frame_sha256"]
+    assert compressor.dict_rounds() != 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("name", ["dict_zero_run_8m_l9", "dict_legacy_12m_l9"])
+def test_dictionary_throughput_floor(compressor, name):
+    """Dictionary mode has no serial cliff: 8 MB with a 64 KiB dictionary and a 200 KB zero run (the
+    same-letter shortcut) and a 12 MB legacy frame with a dictionary both compress at >= 100 MB/s at -9,
+    byte-identical to the reference (host buffers in and out, the second call timed)."""
+    import time
+    case, data, dic = _stream_case(name)
+    compressor.lz4(data[:1 << 20], case["max_chain"], dic, case["legacy"])
+    t0 = time.perf_counter()
+    out = compressor.lz4(data, case["max_chain"], dic, case["legacy"])
+    rate = len(data) / (time.perf_counter() - t0) / 1e6
+    assert inputs.sha(out) == case["frame_sha256"]
+    print(f"{name}: {rate:.1f} MB/s, {compressor.dict_rounds()} rounds")
+    assert rate >= 100.0, rate
 
 
 @pytest.mark.parametrize("chain", [3, 65535])

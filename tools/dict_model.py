@@ -7,7 +7,18 @@ import sys, random
 sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 from smallz4_amd import synth
 W = 65535
+SAME = 19 + 255 * 256  # MaxSameLetter
 def h32(f): return ((f * 48271) & 0xFFFFFFFF) >> 12
+def lcp(d, x, y, cap):
+    """common prefix of d[x:] and d[y:], at most cap (findLongestMatch's phase 2 byte loops)"""
+    if cap <= 0: return 0
+    if d[x:x + cap] == d[y:y + cap]: return cap
+    lo, hi = 0, cap  # d[x:x+lo] == d[y:y+lo], d[x:x+hi] != d[y:y+hi]
+    while hi - lo > 1:
+        m = (lo + hi) // 2
+        if d[x:x + m] == d[y:y + m]: lo = m
+        else: hi = m
+    return lo
 def ld4(d, p): return int.from_bytes(d[p:p+4].ljust(4, b'\0'), 'little')
 
 def serial(data, blocks, dictBack, maxChain):
@@ -19,6 +30,11 @@ def serial(data, blocks, dictBack, maxChain):
         i = back
         while i + 12 <= size:
             pos = start + i
+            # self-matching (smallz4.h:631-643): copy the predecessor's long distance-1 match, no insertion
+            if i > 0 and data[pos] == data[pos - 1] and mdist.get(pos - 1) == 1 and mlen[pos - 1] > SAME:
+                mlen[pos] = mlen[pos - 1] - 1; mdist[pos] = 1
+                i += 1
+                continue
             slot = i & W
             four = ld4(data, pos); h = h32(four)
             cand = last.get(h); last[h] = pos
@@ -53,9 +69,7 @@ def serial(data, blocks, dictBack, maxChain):
                     lo = need - 4
                     while lo > 0 and ld4(data, pos+lo) == ld4(data, c+lo): lo -= 4
                     if lo > 0: continue
-                    hi = need
-                    while hi + 4 <= room and ld4(data, pos+hi) == ld4(data, c+hi): hi += 4
-                    while hi < room and data[pos+hi] == data[c+hi]: hi += 1
+                    hi = need + lcp(data, pos + need, c + need, room - need)
                     bestLen, bestDist = hi, bd
                     steps -= 1
                     if steps == 0: break
@@ -65,7 +79,10 @@ def serial(data, blocks, dictBack, maxChain):
         if end - low > W: low = end - W
     return mlen, mdist, prevH, prevX
 
-def parallel(data, blocks, dictBack, maxChain):
+def parallel(data, blocks, dictBack, maxChain, X=None):
+    """One round of the data-parallel algorithm under an assumed set of same-letter shortcut positions
+    X (position -> inherited match length; those positions are neither inserted nor searched)."""
+    X = X or {}
     nb = len(blocks); cont = 0
     def back(b): return -dictBack if (b == 0 and not cont) else -12
     def dup(b): return b != 0 or cont
@@ -77,8 +94,8 @@ def parallel(data, blocks, dictBack, maxChain):
     for b in range(nb):
         lo, hi = own_lo(b), own_hi(b)
         if hi < lo: continue
-        wlo = max(p0, lo - W)
-        keys = sorted((h32(ld4(data, p)), p) for p in range(wlo, hi + 1))
+        # a block's own insertions suffice: an earlier one is found through the hash table `last`
+        keys = sorted((h32(ld4(data, p)), p) for p in range(lo, hi + 1) if p not in X)
         for j, (h, p) in enumerate(keys):
             if p < lo: continue
             d = None
@@ -90,14 +107,18 @@ def parallel(data, blocks, dictBack, maxChain):
         for j, (h, p) in enumerate(keys):
             if p >= lo and (j + 1 == len(keys) or keys[j+1][0] != h): last[h] = p
     def read_slot(tab, s, b, it):
+        # the latest insertion at or before step it whose block-relative index is s mod 65536; shortcut
+        # positions were never inserted, so their slot keeps the value of 65536 indices earlier
         start = blocks[b][0]
         iw = it - ((it - s) & W)
+        while iw >= back(b) and start + iw in X: iw -= 65536
         if iw >= back(b):
             if iw == -12 and dup(b): return 0
             return tab[start + iw]
         for bb in range(b - 1, -1, -1):
             st, en = blocks[bb]; hi = en - st - 12
             iw = hi - ((hi - s) & W)
+            while iw >= back(bb) and st + iw in X: iw -= 65536
             if iw >= back(bb):
                 if iw == -12 and dup(bb): return 0
                 return tab[st + iw]
@@ -105,7 +126,7 @@ def parallel(data, blocks, dictBack, maxChain):
     for b in range(nb):
         start = blocks[b][0]; low = lowb(b)
         for p in range(own_lo(b), own_hi(b) + 1):
-            it = p - start; first = ph[p]; exact = 0
+            it = p - start; first = ph.get(p, 0) if p not in X else 0; exact = 0
             if first:
                 four = ld4(data, p); h = h32(four); cand = p - first; dist = first; ok = True
                 while True:
@@ -125,6 +146,9 @@ def parallel(data, blocks, dictBack, maxChain):
         start, end = blocks[b]; size = end - start; stop = end - 5
         for i in range(0, size - 12 + 1):
             pos = start + i
+            if pos in X:
+                mlen[pos] = X[pos]; mdist[pos] = 1
+                continue
             if pe[pos] == 0: continue
             bestLen, bestDist, steps = 1, 0, maxChain
             hop = read_slot(pe, pos & W, b, i); bd = 0; room = stop - pos
@@ -138,9 +162,7 @@ def parallel(data, blocks, dictBack, maxChain):
                 lo = need - 4
                 while lo > 0 and ld4(data, pos+lo) == ld4(data, c+lo): lo -= 4
                 if lo > 0: continue
-                hi = need
-                while hi + 4 <= room and ld4(data, pos+hi) == ld4(data, c+hi): hi += 4
-                while hi < room and data[pos+hi] == data[c+hi]: hi += 1
+                hi = need + lcp(data, pos + need, c + need, room - need)
                 bestLen, bestDist = hi, bd
                 steps -= 1
                 if steps == 0: break
@@ -149,6 +171,40 @@ def parallel(data, blocks, dictBack, maxChain):
     cH = [read_slot(ph, s, b, it) for s in range(65536)]
     cX = [read_slot(pe, s, b, it) for s in range(65536)]
     return mlen, mdist, cH, cX
+
+
+def observed_shortcuts(blocks, X, mlen, mdist):
+    """The shortcut positions the reference's loop would take given this round's results: a searched
+    position a (not assumed skipped) with a distance-1 match longer than MaxSameLetter starts
+    a + 1 .. a + La - MaxSameLetter (smallz4.h:631-643); positions assumed skipped but not confirmed have
+    no search result, so they start nothing (the next round searches them)."""
+    Y = {}
+    for (start, end) in blocks:
+        size = end - start
+        i = 1
+        while i + 12 <= size:
+            a = start + i - 1
+            if a in Y: L = Y[a]
+            elif a in X: L = 0
+            else: L = mlen.get(a, 0) if mdist.get(a) == 1 else 0
+            if L > SAME:
+                Y[a + 1] = L - 1
+            i += 1
+    return Y
+
+
+def parallel_sc(data, blocks, dictBack, maxChain, rounds=None):
+    """Rounds of parallel() until the assumed shortcut positions are the ones the results imply; every
+    round settles at least the prefix up to its first disagreement (k_dict_sc_check)."""
+    X = {}
+    for r in range(100):
+        res = parallel(data, blocks, dictBack, maxChain, X)
+        Y = observed_shortcuts(blocks, X, res[0], res[1])
+        if Y == X:
+            if rounds is not None: rounds.append(r + 1)
+            return res
+        X = Y
+    raise RuntimeError("shortcut positions did not settle")
 
 
 # ---- greedy/lazy bookkeeping (k_dict_lz_walk / _fix / _clear): the speculative per-sub-segment walk
