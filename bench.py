@@ -37,8 +37,11 @@ Also reported:
   cpu_baseline   the reference itself on this host (rank 0, every N, after the timed region): one
                  thread per CPU this process may use (affinity mask, capped by the cgroup quota; the
                  count is recorded), and one thread, on a bounded sample
-  stream         sz4_lz4 (the drop-in's host-buffer path: 4 MiB dependent blocks, chunked, PCIe
-                 included) between numpy buffers, 1 GPU, outside the timed region
+  stream         the C++ drop-in (smallz4::lz4 through include/smallz4_amd.hpp, tools/bin/stream_threads):
+                 1 GB, 4 MiB dependent blocks in 64 MiB chunks, callbacks and PCIe in the clock, its own
+                 device footprint; N=1, outside the timed region
+  dictionary     sz4_lz4 with a 64 KiB dictionary: 8 MB at -9 and -6 diffed against the reference, and
+                 8 MB with a 200 KB zero run (the same-letter shortcut) against the reference's frame hash
   shapes         N=1: the other single-GPU-sized configs -- configs[2] (Silesia-shaped, 4 MiB blocks),
                  configs[4]'s 1.25 GiB rank slice, text at 4 MiB blocks, configs[3]'s 125 MB rank slice
                  -- each with ms/step, MB/s, a sampled byte_diff bounded by seconds, and the round trip
@@ -131,7 +134,9 @@ def parse_args(argv=None):
                          "input at N=1 on enwik8 is always diffed)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-decode", action="store_true", help="skip the device round trip (sz4_unlz4_device)")
-    ap.add_argument("--no-stream", action="store_true", help="skip the sz4_lz4 host-buffer leg")
+    ap.add_argument("--no-stream", action="store_true", help="skip the C++ drop-in stream leg")
+    ap.add_argument("--stream-reps", type=int, default=10, help="stream leg: 100 MB repetitions (10 = 1 GB)")
+    ap.add_argument("--no-dict", action="store_true", help="skip the dictionary-mode leg")
     ap.add_argument("--no-shapes", action="store_true", help="skip the other configs (N=1)")
     ap.add_argument("--shape-steps", type=int, default=3)
     ap.add_argument("--shape-verify-seconds", type=float, default=8.0)
@@ -397,6 +402,79 @@ class Runner:
                     "and decode launches with their syncs)", "ms": round(dt * 1e3, 3)}
 
 
+def stream_big_leg(data: bytes, reps: int):
+    """The drop-in stream path in C++: tools/bin/stream_threads (tests/cpp/stream_threads.cpp, built by
+    smallz4_amd/csrc/Makefile) calls smallz4::lz4 through include/smallz4_amd.hpp on `reps` x 100 MB of
+    the benchmark text at -9 -- 4 MiB dependent blocks, 64 MiB chunks, callbacks and PCIe both ways in
+    the clock -- after a first call of one repetition that allocates the pooled context.  A child
+    process: it owns its own context, so its device footprint is its own."""
+    exe = os.path.join(ROOT, "tools", "bin", "stream_threads")
+    if not os.path.exists(exe):
+        return {"skipped": "tools/bin/stream_threads not built"}
+    base = "/tmp/sz4_bench_stream_base.bin"
+    with open(base, "wb") as f:
+        f.write(data[:100_000_000])
+    try:
+        r = subprocess.run([exe, "big", "9", base, str(reps), "/dev/null", "decode"], capture_output=True, text=True,
+                           timeout=400)
+    finally:
+        os.unlink(base)
+    if r.returncode != 0:
+        return {"error": f"exit {r.returncode}", "stderr": r.stderr[-500:]}
+    rec = json.loads(r.stdout.strip().splitlines()[-1])
+    chunks = -(-rec["input_bytes"] // (64 << 20))
+    return {"value": rec["MB/s"], "unit": "MB/s (smallz4::lz4 wall clock: callbacks, PCIe both ways, kernels)",
+            "input_bytes": rec["input_bytes"], "chunks": chunks, "ratio": round(rec["output_bytes"] / rec["input_bytes"], 5),
+            "device_bytes": rec["device_bytes"], "seconds": rec["seconds"],
+            "get_bytes_seconds": rec["get_bytes_seconds"], "send_bytes_seconds": rec["send_bytes_seconds"],
+            "first_call": {"input_bytes": rec["first_call_bytes"], "seconds": rec["first_call_seconds"]},
+            "decode": {"MB/s": rec["decode_MB/s"], "seconds": rec["decode_seconds"], "roundtrip_ok": rec["decode_ok"],
+                       "path": "sz4_unlz4_stream (smallz4cat's unlz4_userPtr interface: getByte per byte, 64 KiB "
+                               "sendBytes) on the frame above, output compared with the input as it arrives"},
+            "path": "tools/bin/stream_threads big: smallz4::lz4 (include/smallz4_amd.hpp) over 4 MiB dependent blocks, "
+                    "64 MiB chunks, level -9, " + f"{reps} x 100 MB of the benchmark text (8 bytes patched per repetition)"}
+
+
+def dictionary_leg(run: Runner, no_verify: bool):
+    """Dictionary mode (smallz4::lz4 with a dictionary, sz4_lz4 between host buffers): 8 MB of text with a
+    64 KiB dictionary at -9 and -6, diffed against the reference (oracle/_ref), and 8 MB with a 200 KB zero
+    run in the middle at -9 (the same-letter shortcut rounds), checked against the reference's own frame
+    hash (tests/golden/streams.json: the reference needs ~15 s for it)."""
+    import hashlib
+    import numpy as np
+    from oracle import pyoracle
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import inputs
+    dic = synth.enwik8_like(65536, seed=82)
+    text = synth.enwik8_like(8_000_000, seed=83)
+    with open(os.path.join(ROOT, "tests", "golden", "streams.json")) as f:
+        fix = {c["name"]: c for c in json.load(f)["cases"]}["dict_zero_run_8m_l9"]
+    cases = [("text_8m_l9", text, dic, 65535, None), ("text_8m_l6", text, dic, 6, None),
+             ("zero_run_8m_l9", inputs.make(fix["input"]), inputs.make(fix["dictionary"]), 65535, fix)]
+    res = {}
+    for name, data, d, chain, want in cases:
+        src = np.frombuffer(data, dtype=np.uint8)
+        dst = np.empty(run.comp._lib.sz4_lz4_bound(src.size, 0), dtype=np.uint8)
+        run.comp.lz4_into(src[:1 << 20], dst, chain, d)
+        t0 = time.perf_counter()
+        size = run.comp.lz4_into(src, dst, chain, d)
+        dt = time.perf_counter() - t0
+        out = dst[:size].tobytes()
+        rec = {"MB/s": round(len(data) / dt / 1e6, 1), "input_bytes": len(data), "dictionary_bytes": len(d),
+               "max_chain": chain, "rounds": run.comp.dict_rounds(), "ratio": round(size / len(data), 5)}
+        if want is not None:
+            rec.update({"byte_diff": 0 if hashlib.sha256(out).hexdigest() == want["frame_sha256"] else -1,
+                        "verified_against": "reference frame SHA-256 (tests/golden/streams.json)"})
+        elif not no_verify and pyoracle.ref_available():
+            ref = pyoracle.ref_lz4(data, chain, d)
+            m = min(len(ref), len(out))
+            rec.update({"byte_diff": int(np.count_nonzero(np.frombuffer(ref[:m], np.uint8) != np.frombuffer(out[:m], np.uint8)))
+                        + abs(len(ref) - len(out)), "verified_against": "reference"})
+        res[name] = rec
+    return {"unit": "MB/s (host buffers in and out, PCIe included; second call timed)", "cases": res,
+            "path": "sz4_lz4 with a dictionary: the data-parallel dictionary finder (sz4_dict.hip), then the usual parse"}
+
+
 def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
     """The other single-GPU-sized configs, each measured, diffed on a bounded sample and round-tripped."""
     torch = run.torch
@@ -502,22 +580,11 @@ def main():
     else:
         frame_bytes, diff, verified, rt_bad = size, ver["byte_diff"], ver["blocks_verified"], 0 if rt_ok else 1
 
-    stream_leg = None
+    stream_leg = dict_leg = None
     if world == 1 and not args.no_stream and nbytes:
-        # the drop-in's host-buffer path (4 MiB dependent blocks, chunked; PCIe included), between
-        # numpy buffers: no Python copies inside the timed call
-        import numpy as np
-        src = np.frombuffer(data[:min(nbytes, 100_000_000)], dtype=np.uint8)
-        dst = np.empty(run.comp._lib.sz4_lz4_bound(src.size, 0), dtype=np.uint8)
-        run.comp.lz4_into(src[:1 << 20], dst, chain)
-        ts = time.perf_counter()
-        ssize = run.comp.lz4_into(src, dst, chain)
-        dts = time.perf_counter() - ts
-        stream_leg = {"value": round(src.size / dts / 1e6, 1), "unit": "MB/s (host buffers in and out, PCIe included)",
-                      "input_bytes": int(src.size), "ratio": round(ssize / src.size, 5),
-                      "path": "sz4_lz4 (smallz4::lz4 stream semantics: 4 MiB dependent blocks, 64 MiB chunks) "
-                              "between numpy buffers",
-                      "device_bytes": run.comp.device_bytes()}
+        stream_leg = stream_big_leg(data, args.stream_reps)
+    if world == 1 and not args.no_dict and args.level == 9:
+        dict_leg = dictionary_leg(run, args.no_verify)
 
     shapes = None
     if world == 1 and not args.no_shapes and args.level == 9 and args.workload == "enwik8" and not args.mb:
@@ -595,6 +662,8 @@ def main():
             rec["unlz4"] = dec
         if stream_leg is not None:
             rec["stream"] = stream_leg
+        if dict_leg is not None:
+            rec["dictionary"] = dict_leg
         if shapes is not None:
             rec["shapes"] = shapes
         # the reference on this host's cores, rank 0, after the timed region (at every N)

@@ -14,10 +14,10 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 400 python3 "$R/bench.py" $EXTRA > "$OUT/bench.json" 2> "$OUT/bench.err"
 cd /tmp
-ARGS="--steps 10 --warmup 3 --no-verify --no-stream --no-shapes --cpu-seconds 0.5 $EXTRA"
+ARGS="--steps 10 --warmup 3 --no-verify --no-stream --no-dict --no-shapes --cpu-seconds 0.5 $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- \
   python3 "$R/bench.py" $ARGS > "$OUT/trace.log" 2>&1
-ARGS="--steps 3 --warmup 1 --no-verify --no-decode --no-stream --no-shapes --cpu-seconds 0.5 $EXTRA"
+ARGS="--steps 3 --warmup 1 --no-verify --no-decode --no-stream --no-dict --no-shapes --cpu-seconds 0.5 $EXTRA"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o bench -- \
   python3 "$R/bench.py" $ARGS > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o bench -- \

@@ -150,7 +150,11 @@ struct sz4_ctx {
   bool ghost = false;
   uint32_t dictCont = 0, dictShift = 0, dictLow0 = 0;
   DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut, unSeq;  // decoder (sz4_unlz4*)
+  DevBuf unSubs, unMasks, unImage;  // decoder split mode: sub-segments, their token-start masks, the u32 image
   std::vector<UnBlock> hUn;
+  std::vector<UnSub> hSub;
+  bool unSplit = false;  // the last planned frame decodes in split mode
+  int unSplitMode = getenv("SZ4_UNLZ4_SPLIT") ? atoi(getenv("SZ4_UNLZ4_SPLIT")) : -1;  // -1 auto, 0 never, 1 always
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
   bool dictSerial = getenv("SZ4_DICT_SERIAL") != nullptr;  // A/B and tests: the in-order replay for every chunk
@@ -184,7 +188,7 @@ struct sz4_ctx {
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
             &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictLz,
             &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
-            &unOut, &unSeq};
+            &unOut, &unSeq, &unSubs, &unMasks, &unImage};
   }
 
   int fail(int code, const char* what, hipError_t e = hipSuccess)
@@ -567,7 +571,38 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   }
   const uint32_t nb = (uint32_t)meta[0];
   c->hUn.resize(nb);
+  c->unSplit = false;
   if (nb) {
+    if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "frame index", e);
+    // split mode when a block is large (one wavefront per block would leave most of the chip idle)
+    uint32_t maxLen = 0;
+    for (const UnBlock& b : c->hUn) maxLen = std::max(maxLen, b.len);
+    c->unSplit = c->unSplitMode == 1 || (c->unSplitMode != 0 && maxLen >= kUnSplitMin);
+  }
+  if (nb && c->unSplit) {
+    c->hSub.clear();
+    for (uint32_t b = 0; b < nb; b++) {
+      UnBlock& B = c->hUn[b];
+      B.subFirst = (uint32_t)c->hSub.size();
+      B.subCount = (B.len + kUnSub - 1) / kUnSub;
+      for (uint32_t k = 0; k < B.subCount; k++) c->hSub.push_back(UnSub{b, k, 0, 0, 0, 0, 0, 0, 0, 0});
+    }
+    const uint32_t nsub = (uint32_t)c->hSub.size();
+    if ((e = c->unSeq.reserve((uint64_t)nsub * 2 * kUnSubCap * sizeof(uint4) + 64)) ||
+        (e = c->unSubs.reserve((uint64_t)nsub * sizeof(UnSub) + 64)) ||
+        (e = c->unMasks.reserve((uint64_t)nsub * (kUnSub / 8) + 64)))
+      return c->fail(SZ4_E_NOMEM, "decoder sequences", e);
+    if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), nb * sizeof(UnBlock), hipMemcpyHostToDevice, s)) ||
+        (e = hipMemcpyAsync(c->unSubs.p, c->hSub.data(), nsub * sizeof(UnSub), hipMemcpyHostToDevice, s)))
+      return c->fail(SZ4_E_DEVICE, "decoder plan", e);
+    launch_unlz4_split_sizes(f, n, c->unBlk.as<UnBlock>(), nb, c->unSubs.as<UnSub>(), nsub, c->unSeq.as<uint4>(),
+                             c->unMasks.as<uint32_t>(), s);
+    if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "block sizes", e);
+  } else if (nb) {
     if ((e = c->unSeq.reserve(unlz4_seq_entries(n, nb) * sizeof(uint4) + 64)))
       return c->fail(SZ4_E_NOMEM, "decoder sequences", e);
     launch_unlz4_sizes(f, n, c->unBlk.as<UnBlock>(), nb, c->unSeq.as<uint4>(), s);
@@ -589,6 +624,14 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
     }
   }
   if (meta[1] != 0 && !ended) return c->fail(SZ4_E_CORRUPT, "invalid or truncated LZ4 frame");
+  // the split image addresses output bytes with 31 bits: a larger output decodes block by block
+  if (c->unSplit && w >= (uint64_t)kUnRef) {
+    const int mode = c->unSplitMode;
+    c->unSplitMode = 0;
+    const int r = unlz4_plan(c, f, n, total, keep, s);
+    c->unSplitMode = mode;
+    return r;
+  }
   *total = w;
   *keep = k;
   return SZ4_OK;
@@ -599,6 +642,32 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
 {
   if (!keep) return SZ4_OK;
   hipError_t e;
+  if (c->unSplit) {
+    // split mode: the u32 image of the output, its references resolved, then packed into `out`
+    const UnBlock& lastB = c->hUn[keep - 1];
+    const uint64_t total = lastB.dst + lastB.size;
+    const uint32_t nsub = lastB.subFirst + lastB.subCount;
+    if ((e = c->unImage.reserve(total * 4 + 64)) || (e = c->unFlags.reserve(64)))
+      return c->fail(SZ4_E_NOMEM, "decoder image", e);
+    uint32_t* flag = c->unFlags.as<uint32_t>();
+    if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), keep * sizeof(UnBlock), hipMemcpyHostToDevice, s)))
+      return c->fail(SZ4_E_DEVICE, "decoder plan", e);
+    launch_unlz4_split_decode(f, n, c->unBlk.as<UnBlock>(), c->unSubs.as<UnSub>(), nsub, c->unSeq.as<uint4>(),
+                              c->unImage.as<uint32_t>(), dict, dl, s);
+    // every pass at least halves the longest reference chain (a chain steps to an earlier sub-segment)
+    for (int pass = 0;; pass++) {
+      uint32_t left = 0;
+      if ((e = hipMemsetAsync(flag, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
+      launch_unlz4_resolve(c->unImage.as<uint32_t>(), total, flag, s);
+      if ((e = hipMemcpyAsync(&left, flag, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+        return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
+      if (!left) break;
+      if (pass > 64) return c->fail(SZ4_E_DEVICE, "decoder references did not resolve");
+    }
+    launch_unlz4_pack(c->unImage.as<uint32_t>(), total, out, s);
+    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "decode", e);
+    return SZ4_OK;
+  }
   const uint64_t flagBytes = ((uint64_t)keep + 2) * 4;
   if ((e = c->unFlags.reserve(flagBytes + 64))) return c->fail(SZ4_E_NOMEM, "decoder flags", e);
   uint32_t* flags = c->unFlags.as<uint32_t>();

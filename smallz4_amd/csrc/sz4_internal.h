@@ -181,12 +181,31 @@ void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
 
 // decoder (sz4_unlz4.hip): one block of an LZ4 frame
 struct UnBlock {
-  uint64_t src;     // payload offset in the frame
-  uint64_t dst;     // output offset (set by the host after the sizes pass)
-  uint64_t size;    // decoded bytes (k_unlz4_sizes), kNone when malformed
-  uint32_t len;     // payload bytes
-  uint32_t stored;  // 1: uncompressed block
-  uint32_t nseq;    // sequences recorded by k_unlz4_sizes
+  uint64_t src;       // payload offset in the frame
+  uint64_t dst;       // output offset (set by the host after the sizes pass)
+  uint64_t size;      // decoded bytes (k_unlz4_sizes / k_unlz4_fix), kNone when malformed
+  uint32_t len;       // payload bytes
+  uint32_t stored;    // 1: uncompressed block
+  uint32_t nseq;      // sequences recorded by k_unlz4_sizes
+  uint32_t subFirst;  // split mode: first sub-segment of the block
+  uint32_t subCount;  // split mode: its sub-segments (ceil(len / kUnSub))
+  uint32_t pad;
+};
+// Split mode (frames with large blocks): every block is cut into sub-segments of kUnSub payload bytes,
+// parsed speculatively from their first byte (k_unlz4_spec), joined to the true token chain per block
+// (k_unlz4_fix), decoded into a u32 value-or-reference image one wavefront per sub-segment
+// (k_unlz4_sub), whose references to earlier sub-segments are resolved by pointer jumping
+// (k_unlz4_resolve) before the bytes are packed (k_unlz4_pack).
+constexpr uint32_t kUnSub = 8192;
+constexpr uint32_t kUnSubCap = kUnSub / 3 + 4;    // sequences one walk over a sub-segment records
+constexpr uint32_t kUnSplitMin = 256u << 10;      // a block of at least this many payload bytes: split mode
+constexpr uint32_t kUnRef = 0x80000000u;          // image word: "same byte as output position (w & ~kUnRef)"
+struct UnSub {
+  uint32_t block, k;        // plan: block index, sub-segment index in the block
+  uint32_t specN, specExit;  // k_unlz4_spec: sequences recorded, block-relative frame offset where it stopped
+  uint32_t specFlags;        // 1: the walk met a malformed sequence at specExit, 2: it reached the block end
+  uint32_t preN, specFrom;   // k_unlz4_fix: sequences re-parsed from the true entry, first speculative one kept
+  uint32_t outRel, outLen;   // k_unlz4_fix: block-relative output offset and decoded bytes
   uint32_t pad;
 };
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s);
@@ -196,5 +215,14 @@ void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb,
 // flags: nb done flags, then the status word, then the ticket (zeroed before the launch)
 void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, const uint4* seq, uint8_t* out,
                          const uint8_t* dict, uint64_t dl, uint32_t* flags, hipStream_t s);
+// split mode: seq holds 2 * kUnSubCap entries per sub-segment (re-parsed prefix, speculative list), masks
+// kUnSub / 32 words per sub-segment
+void launch_unlz4_split_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, UnSub* subs, uint32_t nsub,
+                              uint4* seq, uint32_t* masks, hipStream_t s);
+// image: one u32 per output byte; flag: one u32 (any reference left after a resolve pass)
+void launch_unlz4_split_decode(const uint8_t* f, uint64_t n, const UnBlock* blk, const UnSub* subs, uint32_t nsub,
+                               const uint4* seq, uint32_t* image, const uint8_t* dict, uint64_t dl, hipStream_t s);
+void launch_unlz4_resolve(uint32_t* image, uint64_t total, uint32_t* flag, hipStream_t s);
+void launch_unlz4_pack(const uint32_t* image, uint64_t total, uint8_t* out, hipStream_t s);
 
 }  // namespace sz4

@@ -4391,7 +4391,10 @@ constexpr uint32_t kDpSideStride = kDpSide + kDpSideKeys;
 // ... but only in blocks of more than this many parse segments: in a short block the serial walk is
 // short too, while a range-minimum block's parallel repair reads long match ranges at every position it
 // takes (zeros/urandom, 256 KiB blocks: parse 36.3 ms per 268 MB with it, 10.9 ms without)
-constexpr uint32_t kParRmqMinSegs = 64;
+#ifndef SZ4_PAR_RMQ_MIN
+#define SZ4_PAR_RMQ_MIN 64
+#endif
+constexpr uint32_t kParRmqMinSegs = SZ4_PAR_RMQ_MIN;
 
 template <bool kPar>
 __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sz4_internal.h"
 
 namespace sz4 {
@@ -95,21 +97,40 @@ __device__ __forceinline__ uint4* seq_base(uint4* seqAll, const UnBlock& B, uint
 }
 __device__ __forceinline__ uint32_t seq_cap(const UnBlock& B) { return B.len / 3 + 2; }
 
-// Header walk of one block (smallz4cat.c:212-323): its decoded length, or kNone when it is malformed
-// the way oz_unlz4 rejects it (a length byte, literal run or offset running past the block, offset 0).
-// Every sequence is recorded as (literals, match length, offset, frame offset of the literals from
-// B.src): lane l holds entry (count & ~63) + l until 64 are complete, then one coalesced store.
-__device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane,
-                                uint4* __restrict__ seq, uint32_t* nseq)
+// Header walk of one block (smallz4cat.c:212-323) from block-relative frame offset r0: its decoded
+// length, or kNone when it is malformed the way oz_unlz4 rejects it (a length byte, literal run or
+// offset running past the block, offset 0).  Every sequence is recorded as (literals, match length,
+// offset, frame offset of the literals from B.src): lane l holds entry (count & ~63) + l until 64 are
+// complete, then one coalesced store.  The whole block: r0 = 0, stop = B.len.  A split block's
+// sub-segment (below): the walk stops at its first token start >= stop (W.exit) and, with kMark, sets
+// bit (token start - mb) of the LDS mask for every sequence it parsed; with kMerge, it stops before a
+// token start whose bit is set in that LDS mask (W.merged: the speculative walk of the sub-segment
+// parsed from there on already).
+struct WalkEnd {
+  uint32_t exit;    // block-relative frame offset where the walk stopped
+  uint32_t ns;      // sequences recorded
+  uint32_t merged;  // 1: stopped at a merge bit (exit is that token start)
+  uint32_t end;     // 1: reached the block end
+};
+template <bool kMark, bool kMerge>
+__device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane, uint32_t r0,
+                               uint32_t stop, uint4* __restrict__ seq, uint32_t cap, uint32_t* maskLds, uint32_t mb,
+                               WalkEnd& W)
 {
-  *nseq = 0;
-  if (B.stored) return B.len;  // uncompressed block (smallz4cat.c:329-343)
+  W = WalkEnd{r0, 0u, 0u, 0u};
+  if (B.stored) {  // uncompressed block (smallz4cat.c:329-343)
+    W.exit = B.len;
+    W.end = 1;
+    return B.len;
+  }
   const uint64_t end = B.src + B.len;
-  const uint32_t cap = seq_cap(B);
-  uint64_t r = B.src, w = 0;  // frame cursor; bytes decoded so far
+  uint64_t r = B.src + r0, w = 0;  // frame cursor; bytes decoded so far
   uint32_t ns = 0;
   uint4 buf = make_uint4(0u, 0u, 0u, 0u);
-  auto push = [&](uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel) {
+  auto push = [&](uint32_t tok, uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel) {
+    if constexpr (kMark) {
+      if (lane == 0) atomicOr(&maskLds[(tok - mb) >> 5], 1u << ((tok - mb) & 31));
+    }
     const uint32_t l = ns & 63u;
     buf.x = un_wrlane(buf.x, lits, l);
     buf.y = un_wrlane(buf.y, ml, l);
@@ -118,11 +139,16 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
     ns++;
     if ((ns & 63u) == 0u) seq[ns - 64u + lane] = buf;
   };
+  auto merge_at = [&](uint32_t tok) -> bool {
+    if constexpr (kMerge) return (maskLds[(tok - mb) >> 5] >> ((tok - mb) & 31)) & 1u;
+    return false;
+  };
   Window win{f, n, 0, 0};
   // One sequence byte by byte through the window (smallz4cat.c:212-323): 0 next, 1 block done, 2 malformed.
   // Taken for what the pre-decoded headers below do not cover: extended literal runs, match lengths
   // with more than one extension byte, headers reaching past the register window.
   auto one_seq = [&]() -> int {
+    const uint32_t tokAt = (uint32_t)(r - B.src);
     const uint32_t tok = win.byte(r++, lane);
     uint64_t lits = tok >> 4;
     if (lits == 15) {
@@ -138,7 +164,7 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
     w += lits;
     r += lits;
     if (r == end) {  // the last sequence has literals only
-      push((uint32_t)lits, 0u, 0u, frel);
+      push(tokAt, (uint32_t)lits, 0u, 0u, frel);
       return 1;
     }
     if (r + 2 > end) return 2;
@@ -154,15 +180,19 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
         ml += x;
       } while (x == 255);
     }
-    push((uint32_t)lits, (uint32_t)ml, off, frel);
+    push(tokAt, (uint32_t)lits, (uint32_t)ml, off, frel);
     w += ml;
     return 0;
   };
   // A sequence starting 20 or more bytes before the block end passes every bounds check of one_seq
   // (its header reads at most 18 bytes past the token, its literals end before the block does), so the
   // walk below checks nothing but a zero offset and runs on block-relative 32-bit cursors.
-  const uint32_t fastEnd = B.len > 20u ? B.len - 20u : 0u;
-  while (r < end) {
+  const uint32_t fastEnd = min(B.len > 20u ? B.len - 20u : 0u, stop);
+  while (r < end && (uint32_t)(r - B.src) < stop) {
+    if (kMerge && merge_at((uint32_t)(r - B.src))) {
+      W.merged = 1;
+      break;
+    }
     // Pre-decode a header at every window position q = 4 lane + k: token | offset << 8 | extension
     // byte << 24, or ~0 when the header needs the byte-wise path (literal run >= 15, a second match
     // extension byte, or bytes past the register window).  The walk costs one readlane per sequence.
@@ -183,8 +213,12 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
     }
     const uint32_t wb = (uint32_t)(win.base - B.src);  // window base, block-relative (r >= B.src >= base - 3)
     uint32_t rr = (uint32_t)(r - B.src);
-    bool slow = false;
+    bool slow = false, stopped = false;
     while (rr < fastEnd) {
+      if (kMerge && rr != (uint32_t)(r - B.src) && merge_at(rr)) {
+        stopped = true;
+        break;
+      }
       const uint32_t q = rr - wb;
       if (q >= 192u) break;
       const uint32_t ql = q >> 2;
@@ -196,27 +230,43 @@ __device__ uint64_t unlz4_parse(const uint8_t* __restrict__ f, uint64_t n, const
         break;
       }
       const uint32_t off = (pk >> 8) & 0xFFFFu;
-      if (off == 0) return kNone;  // "invalid offset" (smallz4cat.c:265-267)
+      if (off == 0) {  // "invalid offset" (smallz4cat.c:265-267)
+        W.exit = rr;
+        return kNone;
+      }
       const uint32_t lits = (pk >> 4) & 15u, nib = pk & 15u;
       const uint32_t ml = kMinMatch + nib + (nib == 15u ? pk >> 24 : 0u);
-      push(lits, ml, off, rr + 1u);
+      push(rr, lits, ml, off, rr + 1u);
       w += lits + ml;
       rr += 3u + lits + (nib == 15u ? 1u : 0u);
     }
     r = B.src + rr;
+    if (stopped) continue;  // the loop head sees the merge bit
     if (rr < fastEnd && !slow) continue;  // refill
     // byte-wise: a header the window could not pre-decode, or the block's last 20 bytes
-    if (r >= end) break;
-    if (ns >= cap) return kNone;  // cannot happen in a well-formed block
+    if (r >= end || rr >= stop) break;
+    if (kMerge && merge_at(rr)) {
+      W.merged = 1;
+      break;
+    }
+    if (ns >= cap) {  // cannot happen in a well-formed block
+      W.exit = rr;
+      return kNone;
+    }
     const int e = one_seq();
-    if (e == 2) return kNone;
+    if (e == 2) {
+      W.exit = rr;
+      return kNone;
+    }
     if (e == 1) break;
   }
   if (ns & 63u) {
     const uint32_t b = ns & ~63u;
     if (lane < (ns & 63u)) seq[b + lane] = buf;
   }
-  *nseq = ns;
+  W.exit = (uint32_t)(r - B.src);
+  W.ns = ns;
+  W.end = r >= end ? 1u : 0u;
   return w;
 }
 
@@ -413,11 +463,11 @@ __global__ __launch_bounds__(64) void k_unlz4_sizes(const uint8_t* __restrict__ 
   const uint32_t bi = blockIdx.x, lane = threadIdx.x;
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
-  uint32_t ns = 0;
-  const uint64_t size = unlz4_parse(f, n, B, lane, seq_base(seqAll, B, bi), &ns);
+  WalkEnd W;
+  const uint64_t size = unlz4_walk<false, false>(f, n, B, lane, 0u, B.len, seq_base(seqAll, B, bi), seq_cap(B), nullptr, 0u, W);
   if (lane == 0) {
     blk[bi].size = size;
-    blk[bi].nseq = ns;
+    blk[bi].nseq = W.ns;
   }
 }
 
@@ -445,6 +495,245 @@ __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if (lane == 0) __hip_atomic_store(&done[bi], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ================================================================================================
+// Split mode: blocks decoded by many wavefronts at once (frames of large blocks, e.g. the 4 MiB
+// dependent blocks smallz4::lz4 writes).
+// ================================================================================================
+constexpr uint32_t kSubWords = kUnSub / 32;
+
+__device__ __forceinline__ uint4* sub_pre(uint4* seq, uint32_t g) { return seq + (uint64_t)g * 2 * kUnSubCap; }
+__device__ __forceinline__ uint4* sub_spec(uint4* seq, uint32_t g) { return seq + (uint64_t)g * 2 * kUnSubCap + kUnSubCap; }
+
+// one wavefront per sub-segment: the token chain as if a token started at its first byte, every token
+// start it parsed as a bit.  Wherever the true chain meets one of those starts, the two are the same
+// chain from there on (k_unlz4_fix).
+__global__ __launch_bounds__(64) void k_unlz4_spec(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
+                                                   UnSub* __restrict__ subs, uint32_t nsub, uint4* __restrict__ seq,
+                                                   uint32_t* __restrict__ masks)
+{
+  __shared__ uint32_t mask[kSubWords];
+  const uint32_t g = blockIdx.x, lane = threadIdx.x;
+  if (g >= nsub) return;
+  for (uint32_t w = lane; w < kSubWords; w += 64) mask[w] = 0;
+  __syncthreads();
+  const UnSub U = subs[g];
+  const UnBlock B = blk[U.block];
+  const uint32_t s0 = U.k * kUnSub, s1 = min(s0 + kUnSub, B.len);
+  WalkEnd W{s0, 0u, 0u, 0u};
+  const uint64_t sz = B.stored ? 0ull : unlz4_walk<true, false>(f, n, B, lane, s0, s1, sub_spec(seq, g), kUnSubCap, mask, s0, W);
+  __syncthreads();
+  for (uint32_t w = lane; w < kSubWords; w += 64) masks[(uint64_t)g * kSubWords + w] = mask[w];
+  if (lane == 0) {
+    subs[g].specN = B.stored ? 0u : W.ns;
+    subs[g].specExit = B.stored ? s1 : W.exit;
+    subs[g].specFlags = B.stored ? 0u : ((sz == kNone ? 1u : 0u) | (W.end ? 2u : 0u));
+  }
+}
+
+// one wavefront per block: the true chain enters sub-segment k at the exit of sub-segment k - 1; where
+// the speculative walk of k parsed that token start, its list is the true one from there, else the
+// chain is re-parsed from the entry until it meets a speculative start (or leaves the sub-segment).
+// Output: per sub-segment the re-parsed prefix, the first speculative sequence kept, its output offset
+// and length; per block the decoded length (kNone: malformed, as the whole-block walk would find).
+__global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
+                                                  uint32_t nb, UnSub* __restrict__ subs, uint4* __restrict__ seq,
+                                                  const uint32_t* __restrict__ masks)
+{
+  __shared__ uint32_t mask[kSubWords];
+  const uint32_t bi = blockIdx.x, lane = threadIdx.x;
+  if (bi >= nb) return;
+  const UnBlock B = blk[bi];
+  if (B.subCount == 0) return;  // an empty block (not split)
+  uint32_t t = 0, outRel = 0;
+  bool ok = true, ended = false;
+  for (uint32_t k = 0; k < B.subCount; k++) {
+    const uint32_t g = B.subFirst + k;
+    const uint32_t s0 = k * kUnSub, s1 = min(s0 + kUnSub, B.len);
+    const uint32_t specN = subs[g].specN, specExit = subs[g].specExit, specFlags = subs[g].specFlags;
+    uint32_t preN = 0, specFrom = specN, outLen = 0;
+    if (B.stored) {
+      outLen = s1 - s0;  // an uncompressed block: its bytes as they are
+      t = s1;
+      ended = s1 == B.len;
+    } else if (!ended && t < s1) {
+      for (uint32_t w = lane; w < kSubWords; w += 64) mask[w] = masks[(uint64_t)g * kSubWords + w];
+      __syncthreads();
+      bool merged = (mask[(t - s0) >> 5] >> ((t - s0) & 31)) & 1u;
+      if (!merged) {
+        WalkEnd W;
+        const uint64_t sz = unlz4_walk<false, true>(f, n, B, lane, t, s1, sub_pre(seq, g), kUnSubCap, mask, s0, W);
+        if (sz == kNone) {
+          ok = false;
+          break;
+        }
+        preN = W.ns;
+        outLen = (uint32_t)sz;
+        merged = W.merged != 0;
+        t = W.exit;
+        ended = W.end != 0;
+      }
+      if (merged) {
+        if (specFlags & 1u) {  // the true chain runs into the malformed sequence the walk met
+          ok = false;
+          break;
+        }
+        // rank of the entry among the speculative token starts, and the bytes from there on
+        const uint32_t x = t - s0;
+        uint32_t below = 0;
+        for (uint32_t w = lane; w < kSubWords; w += 64) {
+          const uint32_t m = mask[w];
+          below += w * 32 + 32 <= x ? __popc(m) : (w * 32 < x ? __popc(m & ((1u << (x - w * 32)) - 1u)) : 0u);
+        }
+        for (int d = 32; d >= 1; d >>= 1) below += (uint32_t)__shfl_xor((int)below, d, 64);
+        specFrom = below;
+        const uint4* sp = sub_spec(seq, g);
+        uint32_t bytes = 0;
+        for (uint32_t e = specFrom + lane; e < specN; e += 64) bytes += sp[e].x + sp[e].y;
+        for (int d = 32; d >= 1; d >>= 1) bytes += (uint32_t)__shfl_xor((int)bytes, d, 64);
+        outLen += bytes;
+        t = specExit;
+        ended = (specFlags & 2u) != 0;
+      }
+      __syncthreads();
+    }
+    if (lane == 0) {
+      subs[g].preN = preN;
+      subs[g].specFrom = specFrom;
+      subs[g].outRel = outRel;
+      subs[g].outLen = outLen;
+    }
+    outRel += outLen;
+  }
+  if (lane == 0) blk[bi].size = ok && ended && t == B.len ? (uint64_t)outRel : kNone;
+}
+
+// The decode image: one u32 per output byte, the byte's value (< 256) or kUnRef | p: "the same byte as
+// output position p", for a match byte whose source lies before the sub-segment's own output (another
+// wavefront writes it).  A sub-segment's own earlier bytes are copied as they are (values or
+// references): recent ones through an LDS ring of the last kRingU words, older ones from the image after
+// the wave drained its stores, as in unlz4_decode.
+constexpr uint32_t kRingU = 4096;
+constexpr uint32_t kSyncU = kRingU / 2;
+
+__global__ __launch_bounds__(64) void k_unlz4_sub(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
+                                                  const UnSub* __restrict__ subs, uint32_t nsub, const uint4* __restrict__ seqAll,
+                                                  uint32_t* __restrict__ img, const uint8_t* __restrict__ dict, uint64_t dl)
+{
+  __shared__ uint32_t ring[kRingU];
+  const uint32_t g = blockIdx.x, lane = threadIdx.x;
+  if (g >= nsub) return;
+  const UnSub U = subs[g];
+  const UnBlock B = blk[U.block];
+  const uint64_t D0 = B.dst + U.outRel;  // this sub-segment's first output byte
+  if (B.stored) {
+    const uint64_t s0 = (uint64_t)U.k * kUnSub;
+    for (uint64_t j = lane; j < U.outLen; j += 64) img[D0 + j] = f[B.src + s0 + j];
+    return;
+  }
+  uint64_t P = D0, synced = D0;
+  // the sequences: the re-parsed prefix, then the speculative list from specFrom
+  const uint4* lists[2] = {seqAll + (uint64_t)g * 2 * kUnSubCap, seqAll + (uint64_t)g * 2 * kUnSubCap + kUnSubCap};
+  const uint32_t from[2] = {0u, U.specFrom}, to[2] = {U.preN, U.specN};
+  for (int li = 0; li < 2; li++) {
+    const uint4* seq = lists[li];
+    for (uint32_t b0 = from[li]; b0 < to[li]; b0 += 64) {
+      const uint32_t cnt = to[li] - b0 < 64u ? to[li] - b0 : 64u;
+      const uint4 q = lane < cnt ? seq[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+      const uint32_t tot = q.x + q.y;
+      const uint32_t incl = un_incl_scan_add(tot, lane);
+      const uint32_t rel = incl - tot;  // output offset of the literals from P
+      for (uint32_t j = 0; j < cnt; j++) {
+        const uint32_t L = un_rdlane(q.x, j), M = un_rdlane(q.y, j), off = un_rdlane(q.z, j), fr = un_rdlane(q.w, j);
+        const uint64_t Pj = P + un_rdlane(rel, j);
+        for (uint64_t k = lane; k < L; k += 64) {
+          const uint32_t v = f[B.src + fr + k];
+          img[Pj + k] = v;
+          ring[(Pj + k) & (kRingU - 1u)] = v;
+        }
+        if (!M) continue;
+        const uint64_t Q = Pj + L;
+        const int64_t lo = (int64_t)Q - (int64_t)off;
+        const uint32_t qq = off >= 64u ? off : off * ((64u + off - 1u) / off);
+        for (uint64_t k = 0; k < M; k += 64) {
+          const uint64_t cur = Q + k;
+          if (cur - synced >= kSyncU) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+            synced = cur;
+          }
+          const int64_t ringLo = (int64_t)cur + 64 - (int64_t)kRingU;
+          const uint64_t jj = k + lane;
+          const int64_t src = k == 0 ? lo + (int64_t)(off >= 64u ? lane : lane % off) : (int64_t)(Q + jj) - (int64_t)qq;
+          uint32_t v = 0;
+          if (jj < M) {
+            if (src >= (int64_t)D0 && src >= ringLo) v = ring[(uint64_t)src & (kRingU - 1u)];
+            else if (src >= (int64_t)D0) v = img[src];              // own, drained
+            else if (src >= 0) v = kUnRef | (uint32_t)src;            // another wavefront's byte
+            else if ((uint64_t)(-src) <= dl) v = dict[dl - (uint64_t)(-src)];  // the dictionary's tail
+            // else 0: before the history (oz_unlz4's zero-initialised history)
+            img[Q + jj] = v;
+            ring[(Q + jj) & (kRingU - 1u)] = v;
+          }
+        }
+      }
+      P += un_rdlane(incl, cnt - 1u);
+    }
+  }
+}
+
+// pointer jumping: every reference is replaced by what its target holds (a value, or a reference to an
+// earlier byte); *flag is raised while references remain
+__global__ __launch_bounds__(256) void k_unlz4_resolve(uint32_t* __restrict__ img, uint64_t total, uint32_t* __restrict__ flag)
+{
+  bool left = false;
+  for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (uint64_t)gridDim.x * 256) {
+    const uint32_t v = img[o];
+    if (v & kUnRef) {
+      const uint32_t w = img[v & ~kUnRef];
+      img[o] = w;
+      left |= (w & kUnRef) != 0;
+    }
+  }
+  if (__ballot(left) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_unlz4_pack(const uint32_t* __restrict__ img, uint64_t total, uint8_t* __restrict__ out)
+{
+  for (uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; o < total; o += (uint64_t)gridDim.x * 1024) {
+    if (o + 4 <= total && ((reinterpret_cast<uintptr_t>(out + o) & 3u) == 0)) {
+      const uint4 v = *reinterpret_cast<const uint4*>(img + o);
+      *reinterpret_cast<uint32_t*>(out + o) = (v.x & 0xFFu) | ((v.y & 0xFFu) << 8) | ((v.z & 0xFFu) << 16) | (v.w << 24);
+    } else {
+      for (uint64_t j = o; j < o + 4 && j < total; j++) out[j] = (uint8_t)img[j];
+    }
+  }
+}
+
+void launch_unlz4_split_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, UnSub* subs, uint32_t nsub,
+                              uint4* seq, uint32_t* masks, hipStream_t s)
+{
+  if (nsub) hipLaunchKernelGGL(k_unlz4_spec, dim3(nsub), dim3(64), 0, s, f, n, blk, subs, nsub, seq, masks);
+  if (nb) hipLaunchKernelGGL(k_unlz4_fix, dim3(nb), dim3(64), 0, s, f, n, blk, nb, subs, seq, masks);
+}
+
+void launch_unlz4_split_decode(const uint8_t* f, uint64_t n, const UnBlock* blk, const UnSub* subs, uint32_t nsub,
+                               const uint4* seq, uint32_t* image, const uint8_t* dict, uint64_t dl, hipStream_t s)
+{
+  if (nsub) hipLaunchKernelGGL(k_unlz4_sub, dim3(nsub), dim3(64), 0, s, f, n, blk, subs, nsub, seq, image, dict, dl);
+}
+
+void launch_unlz4_resolve(uint32_t* image, uint64_t total, uint32_t* flag, hipStream_t s)
+{
+  const uint64_t g = std::min<uint64_t>((total + 255) / 256, 8192);
+  if (total) hipLaunchKernelGGL(k_unlz4_resolve, dim3((uint32_t)g), dim3(256), 0, s, image, total, flag);
+}
+
+void launch_unlz4_pack(const uint32_t* image, uint64_t total, uint8_t* out, hipStream_t s)
+{
+  const uint64_t g = std::min<uint64_t>((total + 1023) / 1024, 8192);
+  if (total) hipLaunchKernelGGL(k_unlz4_pack, dim3((uint32_t)g), dim3(256), 0, s, image, total, out);
 }
 
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s)

@@ -3,12 +3,14 @@
 //   stream_threads threads <level> <in1> <out1> [<in2> <out2> ...]
 //       one host thread per (in, out) pair, all calling smallz4::lz4 at the same time (the reference
 //       builds a fresh object per call, smallz4.h:56-64, so concurrent calls must not interfere)
-//   stream_threads big <level> <base> <reps> <out>
+//   stream_threads big <level> <base> <reps> <out> [decode]
 //       one long stream through smallz4::lz4: <base> repeated <reps> times, repetition r with the
 //       8 bytes at offset (r * 7919) % size replaced by r (little endian); prints the library's
 //       device footprint (sz4_device_bytes of the pooled context), the stream's length and its
 //       wall-clock rate (the whole smallz4::lz4 call: callbacks, PCIe both ways, kernels), after a
-//       first call over one repetition that allocates the pooled context's buffers (timed apart)
+//       first call over one repetition that allocates the pooled context's buffers (timed apart);
+//       `decode`: the frame is kept in memory instead and decoded back through sz4_unlz4_stream
+//       (smallz4cat's interface), compared with the input as it arrives, and timed
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -71,6 +73,7 @@ struct Big {
   FILE* out;
   uint64_t sent;
   double getSecs, sendSecs;  // time spent inside the callbacks (the caller's side of the interface)
+  std::vector<unsigned char>* keep = nullptr;  // the frame, kept in memory for the decode check
 };
 struct CallbackClock {
   double* acc;
@@ -103,8 +106,33 @@ void send_big(const void* data, size_t n, void* user)
 {
   Big* b = static_cast<Big*>(user);
   CallbackClock clock{&b->sendSecs};
-  if (n) fwrite(data, 1, n, b->out);
+  if (n && b->out) fwrite(data, 1, n, b->out);
+  if (n && b->keep) b->keep->insert(b->keep->end(), (const unsigned char*)data, (const unsigned char*)data + n);
   b->sent += n;
+}
+
+// decoding the kept frame back (sz4_unlz4_stream, smallz4cat's getByte / sendBytes pattern): the output
+// is compared with the regenerated stream as it arrives
+struct Cat {
+  const std::vector<unsigned char>* frame;
+  uint64_t at;
+  Big gen;       // regenerates the input stream for the comparison
+  uint64_t got;  // output bytes received
+  bool same;
+  std::vector<unsigned char> want;
+};
+unsigned char cat_get(void* user)
+{
+  Cat* c = static_cast<Cat*>(user);
+  return c->at < c->frame->size() ? (*c->frame)[c->at++] : 0;
+}
+void cat_send(const unsigned char* data, unsigned int n, void* user)
+{
+  Cat* c = static_cast<Cat*>(user);
+  c->want.resize(n);
+  const size_t k = get_big(c->want.data(), n, &c->gen);
+  c->same = c->same && k == n && memcmp(c->want.data(), data, n) == 0;
+  c->got += n;
 }
 
 }  // namespace
@@ -139,19 +167,41 @@ int main(int argc, char** argv)
     smallz4::lz4(get_big, send_big, chain, false, &w);
     const double firstSecs = std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     fclose(w.out);
-    Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, fopen(argv[5], "wb"), 0, 0.0, 0.0};
+    const bool decode = argc >= 7 && std::string(argv[6]) == "decode";
+    std::vector<unsigned char> frame;
+    Big b{&base, (uint64_t)atoll(argv[4]), 0, 0, decode ? nullptr : fopen(argv[5], "wb"), 0, 0.0, 0.0};
+    if (decode) {
+      frame.reserve((size_t)(b.reps * base.size() / 2 + (64 << 20)));
+      b.keep = &frame;
+    }
     b.total = b.reps * base.size();
     const auto t0 = std::chrono::steady_clock::now();
     smallz4::lz4(get_big, send_big, chain, false, &b);
     const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    fclose(b.out);
+    if (b.out) fclose(b.out);
+    double catSecs = 0.0;
+    bool catOk = false;
+    if (decode) {
+      // the frame back through the decoder's stream interface (smallz4cat's unlz4_userPtr), compared
+      // with the input as it arrives
+      Cat cat{&frame, 0, Big{&base, b.reps, 0, b.total, nullptr, 0, 0.0, 0.0}, 0, true, {}};
+      sz4_ctx* dc = NULL;
+      sz4_acquire(&dc, getenv("SMALLZ4_AMD_DEVICE") ? atoi(getenv("SMALLZ4_AMD_DEVICE")) : 0);
+      const auto tc = std::chrono::steady_clock::now();
+      const int rc = sz4_unlz4_stream(dc, cat_get, cat_send, NULL, 0, &cat);
+      catSecs = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc).count();
+      sz4_release(dc);
+      catOk = rc == SZ4_OK && cat.same && cat.got == b.total;
+    }
     // the footprint of the pooled context the call used (handed back to the pool, borrowed again)
     sz4_ctx* c = NULL;
     sz4_acquire(&c, getenv("SMALLZ4_AMD_DEVICE") ? atoi(getenv("SMALLZ4_AMD_DEVICE")) : 0);
     printf("{\"input_bytes\": %llu, \"output_bytes\": %llu, \"device_bytes\": %llu, \"seconds\": %.3f, \"MB/s\": %.1f, "
-           "\"get_bytes_seconds\": %.3f, \"send_bytes_seconds\": %.3f, \"first_call_bytes\": %llu, \"first_call_seconds\": %.3f}\n",
+           "\"get_bytes_seconds\": %.3f, \"send_bytes_seconds\": %.3f, \"first_call_bytes\": %llu, \"first_call_seconds\": %.3f, "
+           "\"decode_seconds\": %.3f, \"decode_MB/s\": %.1f, \"decode_ok\": %s}\n",
            (unsigned long long)b.total, (unsigned long long)b.sent, (unsigned long long)sz4_device_bytes(c), secs,
-           b.total / secs / 1e6, b.getSecs, b.sendSecs, (unsigned long long)base.size(), firstSecs);
+           b.total / secs / 1e6, b.getSecs, b.sendSecs, (unsigned long long)base.size(), firstSecs, catSecs,
+           catSecs > 0 ? b.total / catSecs / 1e6 : 0.0, decode ? (catOk ? "true" : "false") : "null");
     sz4_release(c);
     return 0;
   }

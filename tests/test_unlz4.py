@@ -208,3 +208,58 @@ def test_unlz4_c_dropin_program(compressor, tmp_path):
     assert r.stdout == pyoracle.oz_unlz4(frame, dic.read_bytes())
     bad = subprocess.run([str(exe)], input=b"not a frame", capture_output=True)
     assert bad.returncode == 1 and bad.stderr.startswith(b"ERROR: ")
+
+
+@pytest.fixture(scope="module")
+def split():
+    """A context whose decoder runs every frame in split mode (SZ4_UNLZ4_SPLIT=1): blocks cut into
+    8 KiB sub-segments parsed speculatively and joined to the true token chain (k_unlz4_spec /
+    k_unlz4_fix), decoded one wavefront per sub-segment into a value-or-reference image whose references
+    are resolved by pointer jumping (k_unlz4_sub / k_unlz4_resolve / k_unlz4_pack)."""
+    import smallz4_amd
+    os.environ["SZ4_UNLZ4_SPLIT"] = "1"
+    try:
+        c = smallz4_amd.Compressor(device=0)
+    finally:
+        del os.environ["SZ4_UNLZ4_SPLIT"]
+    yield c
+    c.close()
+
+
+def test_unlz4_split_mode_matches_oracle(compressor, split, golden):
+    """Split mode gives the oracle's bytes (or rejects where it rejects) on every frame shape: the golden
+    vectors' frames, independent blocks from 1000 B to 4 MiB at levels 0 / 3 / 9 (stored blocks
+    included), dependent 4 MiB and legacy 8 MiB streams, dictionaries, malformed and mutated frames."""
+    for case in golden:
+        data = inputs.make(case["input"])
+        dictionary = inputs.make(case["dict"]) if "dict" in case else b""
+        check(split, compressor.lz4(data, case["level"], dictionary, bool(case["legacy"])), dictionary)
+    data = synth.enwik8_like(3 << 20, seed=60) + synth.random_bytes(300000, seed=61) + bytes(200000)
+    for bs in (1000, 65536, 1 << 20, 4 << 20):
+        for chain in (0, 3, 65535):
+            assert check(split, compressor.compress_blocks(data, bs, chain)) == data, (bs, chain)
+    d9 = synth.enwik8_like(9 << 20, seed=62) + bytes(3 << 20) + synth.runs(2 << 20, seed=72, max_run=70000)
+    for legacy in (False, True):
+        assert check(split, compressor.lz4(d9, 65535, b"", legacy)) == d9, legacy
+    small = synth.enwik8_like(50000, seed=68)
+    for dictionary in (synth.enwik8_like(20000, seed=69), synth.enwik8_like(90000, seed=70), b"tiny"):
+        check(split, compressor.lz4(small, 65535, dictionary), dictionary)
+    good = compressor.compress_blocks(synth.enwik8_like(70000, seed=64), 65536, 65535)
+    for frame in [good[:k] for k in range(0, len(good), max(1, len(good) // 53))]:
+        check(split, frame)
+    rng = np.random.default_rng(73)
+    base = compressor.lz4(synth.runs(20000, seed=67, max_run=300), 65535)
+    for _ in range(150):
+        f = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            k = int(rng.integers(7, len(f)))
+            f[k] = int(rng.integers(0, 256))
+        check(split, bytes(f))
+
+
+def test_unlz4_split_mode_large_roundtrip(compressor):
+    """The automatic choice: a stream of 4 MiB dependent blocks (smallz4::lz4) takes split mode and
+    decodes back on the device, text plus long runs."""
+    data = synth.silesia_like(24 << 20, seed=74)
+    frame = compressor.lz4(data, 65535)
+    assert compressor.unlz4(frame) == data
