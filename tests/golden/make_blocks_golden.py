@@ -50,6 +50,17 @@ CASES = [
     ("zu_256k", {"gen": "zeros_urandom_range", "lo": 3 * (1 << 24) + 5 * (1 << 20) + 12345, "n": 8 << 20, "seed": 10},
      262144, 65535),
 ]
+# the blocks tests/test_shards.py samples from configs[4]'s full-size slices (the reference needs ~13 s per
+# zeros/urandom block: its chain walk is quadratic in a run), one case per block:
+#   zu_slice_<i>: block i of rank 0's 1.25 GiB slice of the 10 GiB input;  zu_4g_<i>: block i of the
+#   4 GiB one-call test (input from 3 GiB on)
+ZU_BS = 262144
+ZU_SLICE = [0, 1706, 3412, 5118, 5119]
+ZU_4G = [1, 8195, 16383]
+CASES += [(f"zu_slice_{i}", {"gen": "zeros_urandom_range", "lo": i * ZU_BS, "n": ZU_BS, "seed": 10}, ZU_BS, 65535)
+          for i in ZU_SLICE]
+CASES += [(f"zu_4g_{i}", {"gen": "zeros_urandom_range", "lo": (3 << 30) + i * ZU_BS, "n": ZU_BS, "seed": 10}, ZU_BS, 65535)
+          for i in ZU_4G]
 
 
 def _block(args):

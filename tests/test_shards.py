@@ -3,6 +3,10 @@ configs[4] (zeros/urandom, 256 KiB blocks) as the 8-GPU run splits them, one ran
 size.  Blocks are independent, so a rank's part is bare blocks and the rank-ordered parts concatenate
 to the single-GPU frame.  Full-size slices are checked through size-independent properties (device
 round trip, the size-word walk) plus the oracle on a fixed sample of blocks.  Run with -m gpu."""
+import hashlib
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -10,6 +14,7 @@ from oracle import pyoracle
 from smallz4_amd import shard, synth
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _device_roundtrip(compressor, part: bytes, data: bytes):
@@ -31,6 +36,15 @@ def _spans(part: bytes):
         pos += 4 + (word & 0x7FFFFFFF)
     assert pos == len(part)
     return spans
+
+
+def _zu_fixtures(prefix):
+    """{block index: (SHA-256, length)} of the reference's bytes for the sampled configs[4] blocks
+    (tests/golden/make_blocks_golden.py, one single-block case per sampled block)."""
+    with open(os.path.join(ROOT, "tests", "golden", "blocks.json")) as f:
+        cases = json.load(f)["cases"]
+    return {int(c["name"][len(prefix):]): (c["block_sha256"][0], c["block_len"][0])
+            for c in cases if c["name"].startswith(prefix)}
 
 
 def test_two_contexts_shards_concatenate_to_single_frame(compressor):
@@ -65,16 +79,23 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     spans = _spans(part)
     assert len(spans) == (len(data) + bs - 1) // bs
     assert _device_roundtrip(compressor, part, data)
-    # the oracle on a fixed sample of blocks, the first and the last included (a zeros/urandom block
-    # costs the oracle ~13 s -- its chain walk is quadratic in a run -- so that sample is smaller)
-    k = 24 if workload == "enwik9" else 3
-    idx = sorted(set(list(range(0, len(spans), max(1, len(spans) // k))) + [len(spans) - 1]))
-    from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(max_workers=8) as ex:
-        want = list(ex.map(lambda i: pyoracle.oz_block(data[i * bs:(i + 1) * bs], 65535), idx))
-    for i, w in zip(idx, want):
-        o, n = spans[i]
-        assert part[o:o + n] == w, i
+    # a fixed sample of blocks, the first and the last included: enwik9-shaped ones against the oracle,
+    # zeros/urandom ones against the reference's own bytes (tests/golden/blocks.json, zu_slice_*: the
+    # reference needs ~13 s per such block -- its chain walk is quadratic in a run)
+    if workload == "enwik9":
+        idx = sorted(set(list(range(0, len(spans), max(1, len(spans) // 24))) + [len(spans) - 1]))
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(max_workers=8) as ex:
+            want = list(ex.map(lambda i: pyoracle.oz_block(data[i * bs:(i + 1) * bs], 65535), idx))
+        for i, w in zip(idx, want):
+            o, n = spans[i]
+            assert part[o:o + n] == w, i
+    else:
+        fix = _zu_fixtures("zu_slice_")
+        assert sorted(fix) == [0, 1706, 3412, 5118, len(spans) - 1]
+        for i, (sha, n) in fix.items():
+            o, got = spans[i]
+            assert got == n and hashlib.sha256(part[o:o + n]).hexdigest() == sha, i
     # HBM footprint of the context for this slice (grow-only scratch)
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
@@ -114,13 +135,12 @@ def test_batch_4gib_one_call_bounded_memory(compressor):
     assert len(spans) == len(data) // bs
     sizes = compressor.last_block_sizes(len(spans))
     assert sizes == [n for _, n in spans]
-    from concurrent.futures import ThreadPoolExecutor
-    idx = [1, len(spans) // 2 + 3, len(spans) - 1]
-    with ThreadPoolExecutor(max_workers=3) as ex:
-        want = list(ex.map(lambda i: pyoracle.oz_block(data[i * bs:(i + 1) * bs], 65535), idx))
-    for i, w in zip(idx, want):
-        o, n = spans[i]
-        assert part[o:o + n] == w, i
+    # sampled blocks against the reference's own bytes (tests/golden/blocks.json, zu_4g_*)
+    fix = _zu_fixtures("zu_4g_")
+    assert sorted(fix) == [1, len(spans) // 2 + 3, len(spans) - 1]
+    for i, (sha, n) in fix.items():
+        o, got = spans[i]
+        assert got == n and hashlib.sha256(part[o:o + n]).hexdigest() == sha, i
 
 
 def test_batch_pieces_equal_one_run(compressor):
