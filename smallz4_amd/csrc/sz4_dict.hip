@@ -296,8 +296,16 @@ __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__
       int64_t lo = need - 4;
       while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
       if (lo > 0) continue;
-      // phase 2: forward from the first new byte
+      // phase 2: forward from the first new byte; 32 bytes per step while they all agree (the loads of
+      // a step are independent: one latency per 32 bytes in a long run instead of one per 4)
       int64_t hi = need;
+      while (hi + 32 <= room) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int k = 0; k < 32; k += 4) x |= gload4(in, pos + hi + k) ^ gload4(in, c + hi + k);
+        if (x) break;
+        hi += 32;
+      }
       while (hi + 4 <= room && gload4(in, pos + hi) == gload4(in, c + hi)) hi += 4;
       while (hi < room && in[pos + hi] == in[c + hi]) hi++;
       bestLen = (uint32_t)hi;

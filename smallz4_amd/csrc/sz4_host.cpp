@@ -269,7 +269,9 @@ void finish_plan(sz4_ctx* c)
       if (lo == 0) break;
     }
   }
-  c->ldsWindow = true;
+  // SZ4_FIND_HBM=1 (A/B only): the finders read the text from HBM/L2 even when the window fits LDS
+  static const bool forceHbm = getenv("SZ4_FIND_HBM") != nullptr;
+  c->ldsWindow = !forceHbm;
   c->hybridLds = 0;
   for (const Segment& S : c->hSegs) {
     const Block& B = c->hBlocks[S.block];

@@ -410,6 +410,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 
 // k_sort's shared memory (57 KB).  When k_find_sorted sorts its own segment it lives in the window
 // buffer, which is loaded only after the sort.
+#ifndef SZ4_MSD_SORT
+#define SZ4_MSD_SORT 1  // 0: two LSD passes through HBM and a group-start pass (A/B)
+#endif
 struct SortLds {
   uint32_t tile[kSortTile];        // a tile in digit order; the histogram pass's second table; the scan
   uint32_t cnt[kSortWaves][256];   // per wave and digit: count, then offset inside the tile
@@ -418,7 +421,11 @@ struct SortLds {
   uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
   uint32_t wsum[kSortWaves];
   uint32_t nEx;
+  uint32_t bstart[257];            // MSD: first slot of every high-digit bucket
+  uint32_t bnext;                  // MSD: the next bucket a wave takes
 };
+
+static_assert(sizeof(SortLds) <= 65536, "k_find_sorted sorts its segment inside the 64 KiB window buffer");
 
 // exclusive prefix sum over the 256 digits of v (threads 0..255 hold one digit each), result in out
 __device__ __forceinline__ void digit_scan(uint32_t v, uint32_t* out, uint32_t* wsum)
@@ -507,11 +514,24 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     digit_scan(h1, L.gOff[1], L.wsum);
   }
 
-  // 2. two stable passes (low digit first), each tile ranked and reordered in LDS
+  // 2. stable passes, each tile ranked and reordered in LDS.  LSD: the low digit, then the high one.
+  //    MSD: the high digit only (buckets of equal high digit, positions ascending), then every bucket
+  //    is sorted by its low digit by one wavefront (step 3)
+#if SZ4_MSD_SORT
+  if (tid < 256) L.bstart[tid] = L.gOff[1][tid];
+  if (tid == 0) {
+    L.bstart[256] = E;
+    L.bnext = 0;
+  }
+  constexpr uint32_t kPass0 = 1;
+#else
+  constexpr uint32_t kPass0 = 0;
+#endif
   uint32_t* src = reinterpret_cast<uint32_t*>(bufB + S.elemOff);  // pass 1 reads what pass 0 wrote
-  for (uint32_t pass = 0; pass < 2; pass++) {
+  for (uint32_t pass = kPass0; pass < 2; pass++) {
     uint32_t* dst = reinterpret_cast<uint32_t*>((pass == 0 ? bufB : bufA) + S.elemOff);
     const uint32_t sh = pb + 8u * pass;
+    const bool fromText = pass == kPass0;
     for (uint32_t t0 = 0; t0 < E; t0 += kSortTile) {
       const uint32_t tn = E - t0 < kSortTile ? E - t0 : kSortTile;
       for (uint32_t d = tid; d < kSortWaves * 256; d += kSortThreads) (&L.cnt[0][0])[d] = 0;
@@ -522,7 +542,7 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
 #pragma unroll
       for (uint32_t u = 0; u < kSortBatch; u++) {
         const uint32_t i = wb + 64 * u + lane;
-        e[u] = i < t0 + tn ? (pass == 0 ? elem_at(i) : src[i]) : 0u;
+        e[u] = i < t0 + tn ? (fromText ? elem_at(i) : src[i]) : 0u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kSortBatch; u++) {
@@ -579,14 +599,83 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     src = dst;
   }
   // the sorted elements are in bufA; bufB receives the per-slot arrays
-  // 3. hash-group starts: tiles of 1024 consecutive slots, inclusive max-scan of (start slot + 1)
-  //    carried across tiles; every access coalesced
-  uint32_t* s_scan = L.tile;
   const bool small = W <= 65536u;  // == compact_small(S)
   uint16_t* pos16 = reinterpret_cast<uint16_t*>(bufB + S.elemOff);
   uint16_t* gs16 = pos16 + E;
   uint32_t* pos32 = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   uint32_t* gs32 = pos32 + E;
+#if SZ4_MSD_SORT
+  // 3. every high-digit bucket by one wavefront, taken from a counter: its low digits counted, their
+  //    exclusive prefix is each hash group's start (no scan over the segment), and the elements (in
+  //    position order) are ranked stably by ballot, 64 at a time, straight to their final slots
+  {
+    uint32_t* run = L.cnt[wave];                 // per low digit: elements placed so far
+    uint32_t* pre = L.tile + wave * 512u;        // per low digit: first slot inside the bucket
+    const uint32_t lowMask = 255u;
+    while (true) {
+      uint32_t d = 0;
+      if (lane == 0) d = atomicAdd(&L.bnext, 1u);
+      d = rdlane(d, 0);
+      if (d >= 256u) break;
+      const uint32_t b0 = L.bstart[d], b1 = L.bstart[d + 1];
+      if (b0 == b1) continue;
+      for (uint32_t x = lane; x < 256u; x += 64) run[x] = 0;
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&run[(src[i] >> pb) & lowMask], 1u);
+      __builtin_amdgcn_wave_barrier();
+      {
+        // exclusive prefix of the 256 counts: lane l holds digits 4l .. 4l + 3
+        uint32_t c[4], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          c[k] = run[4 * lane + k];
+          sum += c[k];
+        }
+        const uint32_t incl = wave_incl_scan_add(sum);
+        uint32_t acc = incl - sum;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+          pre[4 * lane + k] = acc;
+          run[4 * lane + k] = 0;
+          acc += c[k];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i0 = b0; i0 < b1; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool valid = i < b1;
+        const uint32_t e = valid ? src[i] : 0u;
+        const uint32_t x = (e >> pb) & lowMask;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+          const uint64_t m = __ballot((x >> b) & 1);
+          peers &= ((x >> b) & 1) ? m : ~m;
+        }
+        const uint64_t below = peers & ((1ull << lane) - 1ull);
+        if (valid) {
+          const uint32_t g = b0 + pre[x];
+          const uint32_t slot = g + run[x] + (uint32_t)__popcll(below);
+          const uint32_t rel = e & posMask;
+          if (small) {
+            pos16[slot] = (uint16_t)rel;
+            gs16[slot] = (uint16_t)g;
+          } else {
+            pos32[slot] = rel;
+            gs32[slot] = g;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (valid && below == 0) run[x] += (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+  __syncthreads();
+#else
+  // 3. hash-group starts: tiles of 1024 consecutive slots, inclusive max-scan of (start slot + 1)
+  //    carried across tiles; every access coalesced
+  uint32_t* s_scan = L.tile;
   uint32_t carry = 0;
   // the next tile's element and its predecessor are loaded one tile ahead
   uint32_t eN = tid < E ? src[tid] : 0u, pN = tid > 0 && tid < E ? src[tid - 1] : 0u;
@@ -619,6 +708,7 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     carry = pre;
     __syncthreads();
   }
+#endif
 }
 
 __global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
