@@ -49,6 +49,9 @@ namespace sz4 {
 constexpr uint32_t kDictNoPos = 0xFFFFFFFFu;
 constexpr uint32_t kDictPosBits = 23;  // a block's insertions and the 64 KiB below them: < 2^23 positions
 constexpr uint64_t kDictPosMask = (1ull << kDictPosBits) - 1;
+#ifndef SZ4_DICT_RUNSKIP
+#define SZ4_DICT_RUNSKIP 1  // k_dict_search steps over a run's 1-hop chain stretches (0: A/B)
+#endif
 constexpr uint32_t kDictSkipKey = 1u << kHashBits;  // k_dict_keys: a shortcut position (sorts after every hash)
 constexpr uint32_t kDictSortBits = kHashBits + 1 + kDictPosBits;
 
@@ -66,6 +69,8 @@ struct DictPlan {
   uint32_t legacy;    // independent blocks (tables reset per block, lookback 0)
   const Interval* iv;        // assumed shortcut intervals: block b's at iv[b * kMaxIv], ivCount[b] of them
   const uint32_t* ivCount;
+  const uint2* runTab;       // runs covering whole 64-byte chunks (k_dict_runs), from runBase
+  uint64_t runBase, runChunks;
 
   __host__ __device__ __forceinline__ int64_t back(uint32_t b) const
   {
@@ -137,6 +142,65 @@ __device__ __forceinline__ uint32_t read_slot(const DictPlan& P, const uint16_t*
     }
   }
   return carried[s];
+}
+
+// ---- runs of one byte value (the chains' 1-hop stretches) ------------------------------------------
+// runTab[k] for the 64-byte chunk k of the chunk's staged range (from base, 64-aligned): {first, end} of
+// the run of one byte value that covers the whole chunk, {0, 0} when the chunk is not uniform
+__global__ __launch_bounds__(256) void k_dict_run_flags(const uint8_t* __restrict__ in, uint64_t base, uint64_t nchunks,
+                                                        uint32_t* __restrict__ flag)
+{
+  const uint64_t k = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (k >= nchunks) return;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(in + base + k * 64);
+  const uint32_t v = w[0] & 0xFFu, all = v * 0x01010101u;
+  bool u = true;
+#pragma unroll
+  for (int j = 0; j < 16; j++) u &= w[j] == all;
+  flag[k] = u ? v + 1u : 0u;
+}
+
+// one wavefront per 64 chunks: every run head among them (a uniform chunk whose predecessor is not the
+// same byte) measures its run -- back to its first byte (>= lo), forward over the uniform chunks, then
+// into the chunk after them (< hi) -- and writes it to all its chunks
+__global__ __launch_bounds__(64) void k_dict_runs(const uint8_t* __restrict__ in, uint64_t base, uint64_t nchunks, uint64_t lo,
+                                                  uint64_t hi, const uint32_t* __restrict__ flag, uint2* __restrict__ runTab)
+{
+  const uint32_t lane = threadIdx.x;
+  const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
+  const uint32_t f = k < nchunks ? flag[k] : 0u;
+  const uint32_t fp = k < nchunks && k > 0 ? flag[k - 1] : 0u;
+  if (k < nchunks && f == 0u) runTab[k] = make_uint2(0u, 0u);
+  uint64_t heads = __ballot(f != 0u && fp != f);
+  while (heads) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(heads);
+    heads &= heads - 1;
+    const uint64_t h = (uint64_t)blockIdx.x * 64 + l;
+    const uint32_t v = rdlane(f, l) - 1u;
+    // first byte: the last non-v byte in the 64 before the chunk, + 1
+    const uint64_t c0 = base + h * 64;
+    const int64_t q = (int64_t)c0 - 64 + (int64_t)lane;
+    const uint64_t om = __ballot(q < (int64_t)lo || in[q] != v);  // bytes before lo count as "not v"
+    uint64_t first = om ? c0 - 64 + (uint64_t)(63 - __builtin_clzll(om)) + 1 : c0 - 64;
+    if (first < lo) first = lo;
+    // the uniform chunks of the run, 64 at a time
+    uint64_t j = h + 1;
+    while (true) {
+      const uint64_t jj = j + lane;
+      const bool same = jj < nchunks && flag[jj] == v + 1u;
+      const uint64_t stop = __ballot(!same);
+      if (stop) {
+        j += (uint64_t)__builtin_ctzll(stop);
+        break;
+      }
+      j += 64;
+    }
+    // into chunk j (not uniform v): its leading v bytes
+    const uint64_t e0 = base + j * 64, e = e0 + lane;
+    const uint64_t nm = __ballot(e >= hi || in[e] != v);
+    const uint64_t end = nm ? e0 + (uint64_t)__builtin_ctzll(nm) : e0 + 64;
+    for (uint64_t t = h + lane; t < j; t += 64) runTab[t] = make_uint2((uint32_t)first, (uint32_t)(end < hi ? end : hi));
+  }
 }
 
 __global__ __launch_bounds__(256) void k_dict_begin(uint32_t* __restrict__ last, uint16_t* __restrict__ prevH,
@@ -291,7 +355,35 @@ __global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__
       hop = read_slot(P, pe, prevX0, (uint32_t)((pos - backDist) & kWindow), b, (int64_t)i, B.start, back);
       const int64_t need = (int64_t)bestLen + 1;
       if (need > room) break;
-      const uint64_t c = pos - backDist;
+      uint64_t c = pos - backDist;
+#if SZ4_DICT_RUNSKIP
+      if (hop == 1u && bestLen >= 4u) {
+        // In a run of one byte value v every inserted position's exact predecessor is the one before it,
+        // so the chain steps down the run one position at a time.  Once p holds a match of bestLen and
+        // its byte at bestLen is not v, a candidate c' of the run with c' + need <= run end fails the
+        // first word of phase 1 (bytes need-4 .. need-1: p's differ from v at bestLen, c''s are all v):
+        // the whole stretch is rejected, and the walk continues at its bottom c_j with the hop read there.
+        // Stretch: read at y gives 1 for y in (c_j, c] when y - 1 and y - 2 are inserted positions of
+        // the run's interior (first + 1 .. end - 4) of this block (no shortcut interval among them).
+        const uint64_t rk = (c - P.runBase) >> 6;
+        const uint2 rt = c >= P.runBase && rk < P.runChunks ? P.runTab[rk] : make_uint2(0u, 0u);
+        if (rt.y != 0u && c + (uint64_t)need <= rt.y && c + 3 <= rt.y && in[pos + bestLen] != in[c]) {
+          uint64_t cj = max((uint64_t)rt.x + 2, B.start + 2);
+          const uint32_t niv = P.ivCount[b];
+          const Interval* v = P.iv + (uint64_t)b * kMaxIv;
+          bool inside = false;
+          for (uint32_t k = 0; k < niv; k++) {
+            if (c >= v[k].lo && c < v[k].hi) inside = true;
+            if (v[k].hi <= c && v[k].hi + 2 > cj) cj = v[k].hi + 2;
+          }
+          if (!inside && cj < c && pos - cj <= kWindow) {
+            c = cj;
+            backDist = pos - cj;
+            hop = read_slot(P, pe, prevX0, (uint32_t)(cj & kWindow), b, (int64_t)i, B.start, back);
+          }
+        }
+      }
+#endif
       // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
       int64_t lo = need - 4;
       while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
@@ -668,7 +760,15 @@ int launch_dict_parallel(const DictArgs& A, hipStream_t s)
 {
   const uint32_t nb = A.nb;
   if (!nb) return 0;
-  DictPlan P{A.dBlocks, nb, A.cont, A.dictBack, A.low0, A.legacy ? 1u : 0u, A.iv, A.ivCount};
+  const uint64_t runLo = A.hBlocks[0].start, runHi = A.hBlocks[nb - 1].end;
+  const uint64_t runBase = runLo & ~63ull, runChunks = (runHi - runBase) / 64;
+  DictPlan P{A.dBlocks, nb, A.cont, A.dictBack, A.low0, A.legacy ? 1u : 0u, A.iv, A.ivCount, A.runTab, runBase, runChunks};
+  if (A.buildRuns && runChunks) {
+    hipLaunchKernelGGL(k_dict_run_flags, dim3((uint32_t)((runChunks + 255) / 256)), dim3(256), 0, s, A.in, runBase, runChunks,
+                       A.runFlag);
+    hipLaunchKernelGGL(k_dict_runs, dim3((uint32_t)((runChunks + 63) / 64)), dim3(64), 0, s, A.in, runBase, runChunks, runLo,
+                       runHi, A.runFlag, A.runTab);
+  }
   if (!A.legacy)
     hipLaunchKernelGGL(k_dict_begin, dim3((1u << kHashBits) / 256), dim3(256), 0, s, A.last, A.prevH, A.prevX, A.cont,
                        A.shift);
@@ -712,5 +812,7 @@ int launch_dict_parallel(const DictArgs& A, hipStream_t s)
 }
 
 uint64_t dict_sc_bits_bytes(uint32_t nb, uint64_t maxBlock) { return (uint64_t)nb * ((maxBlock + 63) / 64) * 8 + 64; }
+
+uint64_t dict_run_table_bytes(uint64_t staged) { return (staged / 64 + 2) * (sizeof(uint2) + 4) + 64; }
 
 }  // namespace sz4

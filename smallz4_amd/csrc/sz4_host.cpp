@@ -132,7 +132,7 @@ struct sz4_ctx {
   DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
   DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
-  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
+  DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictRuns, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
   uint32_t dictRounds = 0;  // rounds the last dictionary chunk took (~0u: it fell back to the in-order replay)
   uint64_t dictTempBytes = 0;  // rocPRIM radix sort scratch for dictKeys (queried on first use)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
@@ -186,7 +186,7 @@ struct sz4_ctx {
   {
     return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
             &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictLz,
+            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictRuns, &dictLz,
             &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
             &unOut, &unSeq, &unSubs, &unMasks, &unImage};
   }
@@ -388,7 +388,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       if ((e = c->dictPH.reserve(staged * 2)) || (e = c->dictPE.reserve(staged * 2)) ||
           (e = c->dictKeys.reserve(2 * dict_sort_keys_max() * 8)) || (e = c->dictTemp.reserve(c->dictTempBytes + 64)) ||
           (e = c->dictSc.reserve(dict_sc_bits_bytes(nb, maxBlock))) ||
-          (e = c->dictSnap.reserve(lastBytes + 2 * slotBytes)) ||
+          (e = c->dictSnap.reserve(lastBytes + 2 * slotBytes)) || (e = c->dictRuns.reserve(dict_run_table_bytes(staged))) ||
           (e = c->dictLz.reserve(c->hWalk.size() * dict_lz_mask_bytes_per_walk() + 64)))
         return c->fail(SZ4_E_NOMEM, "dictionary scratch", e);
       // the carried tables as this chunk found them: a round that finds other shortcut intervals starts
@@ -438,7 +438,10 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       A.lzState = c->walkState.as<uint4>();
       A.scBits = c->dictSc.as<uint64_t>();
       A.status = c->status.as<int>();
+      A.runTab = c->dictRuns.as<uint2>();
+      A.runFlag = reinterpret_cast<uint32_t*>(A.runTab + (staged / 64 + 2));
       for (uint32_t round = 0;; round++) {
+        A.buildRuns = round == 0;
         if (round > 0 && ((!c->dictLegacy && (e = tables(false))) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s))))
           return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
         if (launch_dict_parallel(A, s)) return c->fail(SZ4_E_DEVICE, "dictionary kernels");

@@ -147,10 +147,14 @@ struct DictArgs {
   uint4* lzState;
   uint64_t* scBits;
   int* status;
+  uint2* runTab;      // runs covering whole 64-byte chunks: dict_run_table_bytes(staged) with runFlag
+  uint32_t* runFlag;
+  bool buildRuns;     // the first round of a chunk builds the table (the input does not change)
 };
 uint64_t dict_sort_keys_max();
 uint64_t dict_sort_temp_bytes();  // rocPRIM's scratch for dict_sort_keys_max() keys; 0 if the query failed
 uint64_t dict_sc_bits_bytes(uint32_t nb, uint64_t maxBlock);
+uint64_t dict_run_table_bytes(uint64_t staged);
 int launch_dict_parallel(const DictArgs& a, hipStream_t s);
 // greedy/lazy levels: dict_lz_mask_bytes_per_walk() bytes per token-walk sub-segment (lzMasks), one
 // uint4 per sub-segment (lzState)
