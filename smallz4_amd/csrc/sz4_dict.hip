@@ -163,8 +163,57 @@ __global__ __launch_bounds__(256) void k_dict_run_flags(const uint8_t* __restric
 // one wavefront per 64 chunks: every run head among them (a uniform chunk whose predecessor is not the
 // same byte) measures its run -- back to its first byte (>= lo), forward over the uniform chunks, then
 // into the chunk after them (< hi) -- and writes it to all its chunks
+// The first round's guess of the same-letter shortcut intervals, from a run [first, end) of more than
+// MaxSameLetter + 1 bytes: in a block it starts at the run, the first position whose chain begins with
+// the distance-1 candidate is first + 2 (the chain of p starts at the entry of p - 1, and the run's first
+// position has no distance-1 predecessor); a run that comes in from the previous block is met at the
+// block start (its last position before the block is a lookback insertion; legacy frames have none).
+// Appended to the block's list; k_dict_sc checks every guess like any assumed interval.
+__device__ __forceinline__ void dict_guess(const Block* __restrict__ blocks, uint32_t nb, uint32_t legacy, uint64_t first,
+                                           uint64_t end, Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount)
+{
+  if (end - first <= (uint64_t)kSameLetter + 1) return;
+  for (uint32_t b = 0; b < nb; b++) {
+    const Block B = blocks[b];
+    if (B.end <= first || B.start >= end) continue;
+    const uint64_t a = (first < B.start && !legacy) ? B.start : (first > B.start ? first : B.start) + 2;
+    const uint64_t lim = end < B.end - kTailLiterals ? end : B.end - kTailLiterals;
+    if (lim <= a || lim - a <= (uint64_t)kSameLetter || a + kTailNoMatch > B.end) continue;
+    const uint64_t La = lim - a;
+    const uint32_t k = atomicAdd(&ivCount[b], 1u);
+    if (k >= kMaxIv) continue;  // k_dict_sc clamps the count
+    Interval x;
+    x.a = a;
+    x.La = La;
+    x.lo = a + 1;
+    x.hi = a + 1 + (La - kSameLetter);
+    ivAll[(uint64_t)b * kMaxIv + k] = x;
+  }
+}
+
+// the guessed intervals of each block in position order (few: one thread per block)
+__global__ __launch_bounds__(64) void k_dict_guess_sort(uint32_t nb, Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount)
+{
+  const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= nb) return;
+  const uint32_t n = ivCount[b] < kMaxIv ? ivCount[b] : kMaxIv;
+  ivCount[b] = n;
+  Interval* v = ivAll + (uint64_t)b * kMaxIv;
+  for (uint32_t i = 1; i < n; i++) {
+    const Interval x = v[i];
+    uint32_t j = i;
+    while (j > 0 && v[j - 1].lo > x.lo) {
+      v[j] = v[j - 1];
+      j--;
+    }
+    v[j] = x;
+  }
+}
+
 __global__ __launch_bounds__(64) void k_dict_runs(const uint8_t* __restrict__ in, uint64_t base, uint64_t nchunks, uint64_t lo,
-                                                  uint64_t hi, const uint32_t* __restrict__ flag, uint2* __restrict__ runTab)
+                                                  uint64_t hi, const uint32_t* __restrict__ flag, uint2* __restrict__ runTab,
+                                                  const Block* __restrict__ blocks, uint32_t nb, uint32_t legacy,
+                                                  Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount)
 {
   const uint32_t lane = threadIdx.x;
   const uint64_t k = (uint64_t)blockIdx.x * 64 + lane;
@@ -200,6 +249,7 @@ __global__ __launch_bounds__(64) void k_dict_runs(const uint8_t* __restrict__ in
     const uint64_t nm = __ballot(e >= hi || in[e] != v);
     const uint64_t end = nm ? e0 + (uint64_t)__builtin_ctzll(nm) : e0 + 64;
     for (uint64_t t = h + lane; t < j; t += 64) runTab[t] = make_uint2((uint32_t)first, (uint32_t)(end < hi ? end : hi));
+    if (ivAll && lane == 0) dict_guess(blocks, nb, legacy, first, end < hi ? end : hi, ivAll, ivCount);
   }
 }
 
@@ -767,7 +817,8 @@ int launch_dict_parallel(const DictArgs& A, hipStream_t s)
     hipLaunchKernelGGL(k_dict_run_flags, dim3((uint32_t)((runChunks + 255) / 256)), dim3(256), 0, s, A.in, runBase, runChunks,
                        A.runFlag);
     hipLaunchKernelGGL(k_dict_runs, dim3((uint32_t)((runChunks + 63) / 64)), dim3(64), 0, s, A.in, runBase, runChunks, runLo,
-                       runHi, A.runFlag, A.runTab);
+                       runHi, A.runFlag, A.runTab, A.dBlocks, nb, A.legacy ? 1u : 0u, A.guess ? A.iv : nullptr, A.ivCount);
+    if (A.guess) hipLaunchKernelGGL(k_dict_guess_sort, dim3((nb + 63) / 64), dim3(64), 0, s, nb, A.iv, A.ivCount);
   }
   if (!A.legacy)
     hipLaunchKernelGGL(k_dict_begin, dim3((1u << kHashBits) / 256), dim3(256), 0, s, A.last, A.prevH, A.prevX, A.cont,

@@ -134,6 +134,7 @@ struct sz4_ctx {
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictRuns, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
   uint32_t dictRounds = 0;  // rounds the last dictionary chunk took (~0u: it fell back to the in-order replay)
+  bool dictNoGuess = getenv("SZ4_DICT_NO_GUESS") != nullptr;  // A/B: the first round assumes no shortcut interval
   uint64_t dictTempBytes = 0;  // rocPRIM radix sort scratch for dictKeys (queried on first use)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
@@ -442,6 +443,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       A.runFlag = reinterpret_cast<uint32_t*>(A.runTab + (staged / 64 + 2));
       for (uint32_t round = 0;; round++) {
         A.buildRuns = round == 0;
+        A.guess = round == 0 && !c->dictNoGuess;
         if (round > 0 && ((!c->dictLegacy && (e = tables(false))) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s))))
           return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
         if (launch_dict_parallel(A, s)) return c->fail(SZ4_E_DEVICE, "dictionary kernels");
@@ -1084,16 +1086,24 @@ int stream_decompress(sz4_ctx* c, sz4_get_byte get, sz4_send_out send, const uin
   auto decode = [&]() -> int {
     if (frame.size() <= 7) return SZ4_OK;
     for (int k = 0; k < 4; k++) frame.push_back(0);  // end mark
+    // one upload, one plan (its block sizes give the output length), one decode, one download
+    hipError_t e;
+    const uint64_t dl = hist.size(), fl = frame.size();
+    if ((e = c->unFrame.reserve(fl + 64)) || (e = c->unDict.reserve(dl + 64))) return c->fail(SZ4_E_NOMEM, "staging", e);
+    if ((e = hipMemcpy(c->unFrame.p, frame.data(), fl, hipMemcpyHostToDevice)) ||
+        (dl && (e = hipMemcpy(c->unDict.p, hist.data(), dl, hipMemcpyHostToDevice))))
+      return c->fail(SZ4_E_DEVICE, "upload", e);
     uint64_t size = 0;
-    int r = sz4_unlz4(c, frame.data(), frame.size(), hist.empty() ? nullptr : hist.data(), hist.size(), nullptr, 0, &size);
-    if (r == SZ4_E_CAPACITY) {
-      out.resize(size);
-      r = sz4_unlz4(c, frame.data(), frame.size(), hist.empty() ? nullptr : hist.data(), hist.size(), out.data(), size, &size);
-    } else {
-      out.clear();
-    }
-    if (r != SZ4_OK) return r;
+    uint32_t keep = 0;
+    if (int r = unlz4_plan(c, c->unFrame.as<uint8_t>(), fl, &size, &keep, nullptr)) return r;
     out.resize(size);
+    if (size) {
+      if ((e = c->unOut.reserve(size))) return c->fail(SZ4_E_NOMEM, "output", e);
+      if (int r = unlz4_decode(c, c->unFrame.as<uint8_t>(), fl, dl ? c->unDict.as<uint8_t>() : nullptr, dl,
+                               c->unOut.as<uint8_t>(), keep, nullptr))
+        return r;
+      if ((e = hipMemcpy(out.data(), c->unOut.p, size, hipMemcpyDeviceToHost))) return c->fail(SZ4_E_DEVICE, "download", e);
+    }
     // new history: the last 64 KiB of (history, output)
     if (size >= 65536) {
       hist.assign(out.end() - 65536, out.end());

@@ -150,6 +150,7 @@ struct DictArgs {
   uint2* runTab;      // runs covering whole 64-byte chunks: dict_run_table_bytes(staged) with runFlag
   uint32_t* runFlag;
   bool buildRuns;     // the first round of a chunk builds the table (the input does not change)
+  bool guess;         // ... and appends its guess of the shortcut intervals to iv / ivCount (zeroed before)
 };
 uint64_t dict_sort_keys_max();
 uint64_t dict_sort_temp_bytes();  // rocPRIM's scratch for dict_sort_keys_max() keys; 0 if the query failed
