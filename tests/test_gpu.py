@@ -162,22 +162,43 @@ def _skip_into_run(seed):
     return synth.enwik8_like(3000, seed=seed) + r + bytes(10) + b"xyz" + r + bytes(100000) + synth.enwik8_like(20000, seed=seed + 1)
 
 
+def _fixture(name):
+    """A case of tests/golden/streams.json (the reference's own frame, made by make_streams_golden.py):
+    (case, input).  For inputs with long zero runs, where the reference's chain walk is quadratic."""
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "streams.json")) as f:
+        case = {c["name"]: c for c in json.load(f)["cases"]}[name]
+    data = inputs.make(case["input"])
+    assert inputs.sha(data) == case["input_sha256"]
+    return case, data
+
+
+def _matches_fixture(frame, case):
+    return len(frame) == case["frame_len"] and inputs.sha(frame) == case["frame_sha256"]
+
+
 @pytest.mark.parametrize("chain", [1, 2, 3, 4, 5, 6])
 def test_greedy_lazy_long_runs(compressor, chain):
     """Greedy/lazy levels on same-letter runs > 65299 bytes: k_prep verifies the assumed shortcut
-    intervals and the pipeline reruns until they match the reference's loop (smallz4.h:631-643, 726-744)."""
-    for data, bs in ((_skip_into_run(40), 262144), (synth.enwik8_like(30000, seed=41) + bytes(150000), 262144),
-                     (bytes(70000) + synth.enwik8_like(5000, seed=42) + bytes(90000), 1 << 20)):
-        assert compressor.compress_blocks(data, bs, chain) == expected_frame(data, bs, chain)
-    data = synth.enwik8_like((4 << 20) - 40000, seed=43) + bytes(140000) + synth.enwik8_like(10000, seed=44)
-    assert compressor.lz4(data, chain) == pyoracle.oz_lz4(data, chain)
+    intervals and the pipeline reruns until they match the reference's loop (smallz4.h:631-643, 726-744).
+    Against the reference's own frames (tests/golden/streams.json)."""
+    for name, data0, bs in ((f"gl_skip_into_run_l{chain}", _skip_into_run(40), 262144),
+                            (f"gl_runs_a_l{chain}", synth.enwik8_like(30000, seed=41) + bytes(150000), 262144),
+                            (f"gl_runs_b_l{chain}", bytes(70000) + synth.enwik8_like(5000, seed=42) + bytes(90000), 1 << 20)):
+        case, data = _fixture(name)
+        assert data == data0 and case["block_size"] == bs
+        assert _matches_fixture(compressor.compress_blocks(data, bs, chain), case), name
+    case, data = _fixture(f"gl_runs_4m_l{chain}")
+    assert data == synth.enwik8_like((4 << 20) - 40000, seed=43) + bytes(140000) + synth.enwik8_like(10000, seed=44)
+    assert _matches_fixture(compressor.lz4(data, chain), case)
 
 
 def test_blocks_long_run_shortcut(compressor):
     # a same-letter run longer than MaxSameLetter inside one 256 KiB block (smallz4.h:631-643)
-    data = synth.enwik8_like(30000, seed=9) + bytes(150000) + synth.enwik8_like(82144, seed=10)
     for chain in (7, 8, 65535):
-        assert compressor.compress_blocks(data, 262144, chain) == expected_frame(data, 262144, chain)
+        case, data = _fixture(f"shortcut_256k_l{chain}")
+        assert data == synth.enwik8_like(30000, seed=9) + bytes(150000) + synth.enwik8_like(82144, seed=10)
+        assert _matches_fixture(compressor.compress_blocks(data, 262144, chain), case), chain
 
 
 def test_finder_intermediate_matches(compressor):
