@@ -847,6 +847,9 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 #define SZ4_LPF_LONG 0
 #endif
 constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
+#ifndef SZ4_LPF_LOCAL
+#define SZ4_LPF_LOCAL 0  // 1: the LPF routing decided from the chunk's own lanes instead of 8 probes (A/B)
+#endif
 #ifndef SZ4_LPF_SLACK
 #define SZ4_LPF_SLACK 1
 #endif
@@ -1019,11 +1022,34 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     // LPF targets in blocks above 64 KiB only: a 64 KiB block's groups are small, and text gains nothing
     // there that would pay for k_find_big's pass over the segment
     const bool lpfBlock = B.end - B.start > 65536u;
+#if SZ4_LPF_LOCAL
+    // the LPF decision from the chunk itself: a target of the group that began before the chunk (more than
+    // kLpfMin members below it) whose preceding byte at least 3/4 of that group's lanes in the chunk share
+    // (their positions are the group's nearest to the target) -- no probes into the group below
+    bool lpfLocal = false;
+    if (unlimited && cut == kNone && lpfOk && lpfBlock) {
+      const bool cand = active && slot - gs > kLpfMin && p > predLoF;
+      const bool inGroup = inChunk && gs == rdlane(gs, 0) && gs < first;
+      const uint32_t cls = cand ? (src.ld4(p - 1) & 0xFFu) : 0x100u;
+      uint64_t peers = __ballot(inGroup && cand);
+      const uint32_t nGroup = (uint32_t)__popcll(__ballot(inGroup));
+#pragma unroll
+      for (int b = 0; b < 9; b++) {
+        const uint64_t m = __ballot((cls >> b) & 1u);
+        peers &= ((cls >> b) & 1u) ? m : ~m;
+      }
+      lpfLocal = cand && inGroup && nGroup >= 16u && (uint32_t)__popcll(peers) * 4u >= 3u * nGroup;
+    }
+#endif
     const bool big = unlimited && cut == kNone && active &&
                      (slot - gs > kBigGroup ||
                       (lpfOk && ((run_key(me0) && slot - gs > (lpfBlock ? kBigRunL : kBigRun)) ||
+#if SZ4_LPF_LOCAL
+                                 lpfLocal)));
+#else
                                  (lpfBlock && slot - gs > kLpfMin && p > predLoF &&
                                   lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, me1, me2, src)))));
+#endif
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;

@@ -401,7 +401,15 @@ __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ 
                                                     uint64_t maxBlocks, uint64_t* __restrict__ meta)
 {
   if (threadIdx.x != 0) return;
-  auto rd32 = [&](uint64_t o) {
+  // a size word at any offset: two aligned dwords when the frame is 4-byte aligned and they lie inside
+  // it (one load latency per hop of the chain), else byte by byte
+  const bool aligned = (reinterpret_cast<uintptr_t>(f) & 3u) == 0;
+  auto rd32 = [&](uint64_t o) -> uint32_t {
+    const uint64_t a = o & ~3ull;
+    if (aligned && a + 8 <= n) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(f + a);
+      return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
+    }
     return (uint32_t)f[o] | ((uint32_t)f[o + 1] << 8) | ((uint32_t)f[o + 2] << 16) | ((uint32_t)f[o + 3] << 24);
   };
   uint64_t nb = 0, st = 0, r = 4;
