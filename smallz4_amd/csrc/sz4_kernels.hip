@@ -848,7 +848,7 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
 #endif
 constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
 #ifndef SZ4_LPF_LOCAL
-#define SZ4_LPF_LOCAL 0  // 1: the LPF routing decided from the chunk's own lanes instead of 8 probes (A/B)
+#define SZ4_LPF_LOCAL 1  // 0: the LPF routing decided by 8 probes into the group below the target (A/B)
 #endif
 #ifndef SZ4_LPF_SLACK
 #define SZ4_LPF_SLACK 1
