@@ -494,7 +494,7 @@ def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
         steps = args.shape_steps
         elapsed, stages, size, out, t_in = run.compress(data, bs, chain, steps, 1, "none")
         part = out[:size].cpu().numpy().tobytes()
-        rt_ok, _ = run.roundtrip(out, size, "none", t_in, reps=1)
+        rt_ok, rt = run.roundtrip(out, size, "none", t_in, reps=2)
         del out, t_in
         torch.cuda.empty_cache()
         rec = {"config": f"{wl} ({WORKLOADS[wl][0]}): {len(data) / 1e6:g} MB as independent {bs}-byte blocks, "
@@ -502,7 +502,8 @@ def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
                "input_bytes": len(data), "MB/s": round(len(data) * steps / elapsed / 1e6, 2),
                "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps, "warmup": 1,
                "compression_ratio": round((size + 11) / len(data), 5), "roundtrip_ok": rt_ok,
-               "stages_ms": {k: round(v, 3) for k, v in stages.items()}, "generate_s": round(gen_s, 1)}
+               "stages_ms": {k: round(v, 3) for k, v in stages.items()}, "generate_s": round(gen_s, 1),
+               "unlz4": rt}
         if not args.no_verify:
             rec.update(verify_sample(part, data, bs, chain, args.verify_threads, args.shape_verify_seconds, every=False))
         res[label] = rec
