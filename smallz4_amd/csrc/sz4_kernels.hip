@@ -166,6 +166,15 @@ constexpr int kRowHalfMirror = 0x141;
 constexpr int kRowMirror = 0x140;
 constexpr int kRowShr = 0x110;        // + n
 constexpr int kWaveShr1 = 0x138;      // wave_shr:1 (whole 64-lane wavefront)
+constexpr int kRowBcast15 = 0x142;    // lane 15 of each row to the next row
+constexpr int kRowBcast31 = 0x143;    // lane 31 to rows 2 and 3
+
+// DPP into the rows of kRowMask only; the other rows (and lanes without a source) keep `old`
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp_rows(uint32_t old, uint32_t v)
+{
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, kCtrl, kRowMask, 0xF, false);
+}
 
 
 // every lane receives the min / max of its 16-lane row
@@ -410,6 +419,15 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 
 // k_sort's shared memory (57 KB).  When k_find_sorted sorts its own segment it lives in the window
 // buffer, which is loaded only after the sort.
+#ifndef SZ4_DP_VEC
+#define SZ4_DP_VEC 1  // 0: the parse's fast batches one position at a time in the scalar unit (A/B)
+#endif
+constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
+
+#ifndef SZ4_WALK_VEC
+#define SZ4_WALK_VEC 1  // 0: the forward walk one match at a time in the scalar unit (A/B)
+#endif
+
 #ifndef SZ4_MSD_SORT
 #define SZ4_MSD_SORT 1  // 0: two LSD passes through HBM and a group-start pass (A/B)
 #endif
@@ -4132,6 +4150,9 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
                                                              uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll)
 {
   __shared__ uint32_t rings[kSpecWaves][kRing];
+#if SZ4_DP_VEC
+  __shared__ uint32_t fastRec[kSpecWaves][128];  // the row-transposed batches' keys and costs (biased)
+#endif
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform
   const uint32_t segIdx = blockIdx.x * kSpecWaves + wave;
   if (segIdx >= ndp) return;  // whole wavefronts only; the waves never synchronize
@@ -4270,6 +4291,81 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
     if (cnt == 64u) {
       const uint32_t rowMax = row_max(myL);
       const uint32_t cmax = max(max(rdlane(rowMax, 0), rdlane(rowMax, 16)), max(rdlane(rowMax, 32), rdlane(rowMax, 48)));
+#if SZ4_DP_VEC
+      if (cmax <= 64u && lits + 4u < litBump) {
+        // Row-transposed batches.  The window is held as lane 16q + j = cost[i0 + 4j + 4 - q] << 6, so the
+        // next batch's window is one DPP row shift with the four new costs entering lane 0 of their own
+        // row.  The four positions' candidate keys (64 lanes each) are folded into one register by two
+        // permlane32 swaps and one permlane16 swap (row r = position i0 - r), reduced inside the rows, and
+        // the literal chain c_r = min(c_{r-1} + 1, mc_r) is a prefix minimum over the rows of mc_r - r
+        // (two row broadcasts).  Costs and keys are recorded in LDS by each row's lane 0; the scalar unit
+        // keeps only the literal-run length.
+        const uint32_t q = lane >> 4, j = lane & 15u, o = 4u * j + 4u - q;  // o = cost offset in this lane
+        uint32_t kP[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const uint32_t len = o + (uint32_t)r;
+          // biased by -r << 6 so that (key >> 6) is mc_r - r; len < 4: far above every valid key
+          kP[r] = len < (uint32_t)kMinMatch ? 0x80000000u
+                                            : (((3u + (len >= 19u ? 1u : 0u)) << 6) + (64u - len) - ((uint32_t)r << 6));
+        }
+        // natural -> transposed window: lane 16q + j reads natural lane 4j + 3 - q
+        uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((o - 1u) << 2), (int)win);
+        uint32_t* rec = fastRec[wave];
+        const uint32_t rowBias = q << 6;
+        auto batch = [&](uint32_t t) {
+          uint32_t kv[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int32_t Lr = (int32_t)rdlane(myL, t + (uint32_t)r);
+            kv[r] = (int32_t)o <= Lr - r ? w + kP[r] : kKeyNone;
+          }
+          // fold: rows 0, 1 of X = position 0, rows 2, 3 = position 2; Y likewise positions 1, 3
+          auto x = __builtin_amdgcn_permlane32_swap(kv[0], kv[2], false, false);
+          auto y = __builtin_amdgcn_permlane32_swap(kv[1], kv[3], false, false);
+          const uint32_t X = min(x[0], x[1]), Y = min(y[0], y[1]);
+          auto z = __builtin_amdgcn_permlane16_swap(X, Y, false, false);
+          const uint32_t key = row_min(min(z[0], z[1]));  // row r: position i0 - r, biased
+          const uint32_t a = key >> 6;                    // mc_r - r
+          uint32_t pm = min(a, dpp_rows<kRowBcast15, 0xA>(0xFFFFFFFFu, a));
+          pm = min(pm, dpp_rows<kRowBcast31, 0xC>(0xFFFFFFFFu, pm));
+          const uint32_t cp = min(pm, costNext + 1u);     // c_r - r
+          const uint64_t use = __ballot(cp == a) & 0x0001000100010001ull;
+          if ((lane & 15u) == 0) {
+            rec[t + q] = key;
+            rec[64 + t + q] = cp;
+          }
+          costNext = rdlane(cp, 48) + 3u;
+          if (use) {
+            lits = 3u - ((63u - (uint32_t)__builtin_clzll(use)) >> 4);
+            litBump = 15u;
+          } else {
+            lits += 4u;
+          }
+          // next window: rows shift by one lane, lane 0 of row r takes c_r << 6
+          w = (uint32_t)__builtin_amdgcn_update_dpp((int)((cp << 6) + rowBias), (int)w, kRowShr + 1, 0xF, 0xF, false);
+        };
+        uint32_t t = 0;
+#pragma unroll
+        for (uint32_t tb = 0; tb < 64; tb += 4) {
+          batch(tb);
+          t = tb + 4u;
+          if (tb + 4u < 64u && lits + 4u >= litBump) break;
+        }
+        tFast = t;
+        // transposed -> natural: lane l = cost[i0 + 1 + l] is transposed lane 16 (3 - (l & 3)) + (l >> 2)
+        win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (3u - (lane & 3u))) + (lane >> 2)) << 2), (int)w);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t rk = rec[lane], rc = rec[64 + lane];
+        if (lane < tFast) {
+          kvBuf = rk + ((lane & 3u) << 6);
+          mcBuf = rc + (lane & 3u);
+        }
+        chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
+      }
+#else
       auto fast = [&](auto smallTag) -> uint32_t {
         constexpr bool kSmall = decltype(smallTag)::value;  // every length <= 16: row 0 holds every candidate
 #pragma unroll
@@ -4311,6 +4407,7 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
       if (cmax <= 16u) tFast = fast(std::integral_constant<bool, true>());
       else if (cmax <= 64u) tFast = fast(std::integral_constant<bool, false>());
       if (tFast) chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
+#endif
     }
     for (uint32_t t = tFast; t < 64; t += 4) {
       const int32_t i0 = hi - (int32_t)t;
@@ -4950,6 +5047,69 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   const uint32_t a = ws.y * kWalkSeg;
   const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
 
+#if SZ4_WALK_VEC
+  // A window of 64 positions at a time, on the vector unit: lane l steps to l + max(1, chosen[l])
+  // (F1, 64 = out of the window), F2 .. F32 by doubling (ds_bpermute), and every lane finds the last
+  // path position at or below itself by binary lifting from the entry; the lanes that find themselves
+  // are the path, its matches go to the slots compacted by mbcnt.  A window without a match from the
+  // entry on is skipped with one ballot.
+  auto ldw = [&](uint32_t b) -> uint32_t {
+    const uint32_t i = b + lane;
+    return L[i < n ? i : n - 1u];
+  };
+  uint32_t wbase = a, e = 0, m = 0, exitPos = aNext;
+  uint32_t wL = ldw(a), nL = ldw(a + 64);
+  while (true) {
+    const uint32_t lim = aNext - wbase < 64u ? aNext - wbase : 64u;  // window positions before aNext
+    const uint32_t len = wbase + lane < n && wL > 1u ? wL : 1u;
+    const uint64_t mm = __ballot(len > 1u && lane >= e && lane < lim);
+    uint32_t next, lastLen = 1;
+    if (mm == 0) {
+      next = wbase + lim;  // literals carry the path out of the window (or to aNext)
+    } else {
+      uint32_t F[6];
+      F[0] = lane + len < 64u ? lane + len : 64u;
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(F[k - 1] << 2), (int)F[k - 1]);
+        F[k] = F[k - 1] >= 64u ? 64u : g;
+      }
+      uint32_t x = e;
+      {
+        const uint32_t y = rdlane(F[5], e);
+        x = y <= lane ? y : x;
+      }
+#pragma unroll
+      for (int k = 4; k >= 0; k--) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)F[k]);
+        x = y <= lane ? y : x;
+      }
+      const bool rec = x == lane && len > 1u && lane < lim;
+      const uint64_t rb = __ballot(rec);
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(rb);
+      if (m + cnt > kWalkCap) {
+        if (lane == 0) atomicOr(status, kStInvariant);
+        break;
+      }
+      if (rec) slots[m + __builtin_amdgcn_mbcnt_hi((uint32_t)(rb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rb, 0u))] = wbase + lane;
+      m += cnt;
+      const uint32_t p = rdlane(x, lim - 1u);  // the last path position before lim
+      lastLen = rdlane(len, p);
+      next = wbase + p + lastLen;
+    }
+    if (next >= aNext) {
+      exitPos = lastLen > 1u ? next : aNext;
+      break;
+    }
+    const uint32_t nb = next & ~63u;
+    wL = nb == wbase + 64u ? nL : ldw(nb);
+    nL = ldw(nb + 64u);
+    wbase = nb;
+    e = next & 63u;
+  }
+  if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, exitPos, 0u);
+}
+#else
   uint32_t pos = a, wbase = a, m = 0, slotBuf = 0;
   bool viaMatch = false;
   uint32_t wL, xL1, xL2, xL3;
@@ -5016,6 +5176,7 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   if (lane < (m & 63u)) slots[(m & ~63u) + lane] = slotBuf;
   if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, viaMatch ? pos : aNext, 0u);
 }
+#endif
 
 // Sub-segment repair.  Sub-segment k's walk is exact when the true path enters it at a position the
 // speculative walk also visits; otherwise the path is walked again from its true entry until it meets
