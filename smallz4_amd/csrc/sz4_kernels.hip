@@ -424,6 +424,10 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 #endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
+#ifndef SZ4_HIT2
+#define SZ4_HIT2 1  // 0: round 3's filter-hit code (masks from need bytes, satOk applied afterwards)
+#endif
+
 #ifndef SZ4_WALK_VEC
 #define SZ4_WALK_VEC 1  // 0: the forward walk one match at a time in the scalar unit (A/B)
 #endif
@@ -1117,7 +1121,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // key = prefix << 17 | slot (slots grow with position inside a group), order-free and
       // branch-free.  Prefixes are exact up to 12 bytes; candidates reaching 12 are queued and
       // extended from the text in batches of 64 (one per lane).
-      uint32_t bestKey = 0;
+      uint32_t bestKey = SZ4_HIT2 ? 3u << 17 : 0u;  // length 3: no match yet
       uint32_t qn = 0;
       bool walk = false;  // phase 1: this lane still takes candidates inside the chunk
       satBest[lane] = 0;
@@ -1167,6 +1171,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       };
       // lanes whose match can still grow past 12 bytes
       const uint64_t satOk = __ballot(limit > 12u);
+      const uint32_t noGrow = limit > 12u ? 0u : 1u;
       // the same for a candidate every lane takes: its key, and x0 | x1 | x2 (0: all 12 bytes equal)
       auto score = [&](uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
         const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
@@ -1219,6 +1224,18 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // candidates arrive nearest first (slots descend), so one can raise bestKey only with a longer
       // prefix: it must match the first bestLen + 1 bytes (all 12 once a lane holds 12 or its cap).
       // m1 / m2 mask bytes 4..11 of that need; the exact prefix is computed on a hit only
+#if SZ4_HIT2
+      // bestKey starts at length 3 (no match): the bytes to test past the first four are 8 (len - 3),
+      // all of them once len reaches the cap -- as 63 mask bits: bit 63 of x2:x1 untested, which only
+      // lets a rare candidate through the filter whose exact prefix then does not count
+      auto setMasks = [&]() {
+        const uint32_t len = bestKey >> 17;
+        const uint32_t bits = len >= cap12 ? 63u : min(8u * len - 24u, 63u);
+        const uint64_t mk = (1ull << bits) - 1ull;
+        m1 = (uint32_t)mk;
+        m2 = (uint32_t)(mk >> 32);
+      };
+#else
       auto setMasks = [&]() {
         const uint32_t len = bestKey >> 17;
         const uint32_t need = len >= cap12 ? 12u : max(len + 1u, 4u);  // 4..12
@@ -1226,6 +1243,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         m1 = (uint32_t)mk;
         m2 = (uint32_t)(mk >> 32);
       };
+#endif
       auto filt = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
         return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
       };
@@ -1233,9 +1251,29 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #if SZ4_DIAG == 3
         dBi++;  // hit branches (wave-level)
 #endif
+#if SZ4_HIT2
+        const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        const uint32_t lcp = min(4u + (z >> 3), cap12);
+        const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+        setMasks();
+        // queued: 12 bytes equal, and the match may grow past them
+        const bool me = mine && (x0 | x1 | x2 | noGrow) == 0u;
+        const uint64_t sat = __ballot(me);
+        if (sat) {
+          const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
+          if (me) satQ[at] = (lane << 17) | cs;
+          qn += (uint32_t)__builtin_popcountll(sat);
+          if (qn >= 64) flush();
+        }
+#else
         const uint32_t x = scoreIf(mine, cs, k0, k1, k2);
         setMasks();
         enqueue(__ballot(x == 0u) & satOk, cs);
+#endif
       };
       setMasks();
 #endif
@@ -4150,9 +4188,6 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
                                                              uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll)
 {
   __shared__ uint32_t rings[kSpecWaves][kRing];
-#if SZ4_DP_VEC
-  __shared__ uint32_t fastRec[kSpecWaves][128];  // the row-transposed batches' keys and costs (biased)
-#endif
   const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // uniform
   const uint32_t segIdx = blockIdx.x * kSpecWaves + wave;
   if (segIdx >= ndp) return;  // whole wavefronts only; the waves never synchronize
@@ -4298,8 +4333,8 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
         // row.  The four positions' candidate keys (64 lanes each) are folded into one register by two
         // permlane32 swaps and one permlane16 swap (row r = position i0 - r), reduced inside the rows, and
         // the literal chain c_r = min(c_{r-1} + 1, mc_r) is a prefix minimum over the rows of mc_r - r
-        // (two row broadcasts).  Costs and keys are recorded in LDS by each row's lane 0; the scalar unit
-        // keeps only the literal-run length.
+        // (two row broadcasts).  A batch's keys shift into their rows like the window, its costs stay in the window;
+        // the scalar unit keeps only the literal-run length.
         const uint32_t q = lane >> 4, j = lane & 15u, o = 4u * j + 4u - q;  // o = cost offset in this lane
         uint32_t kP[4];
 #pragma unroll
@@ -4311,13 +4346,18 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
         }
         // natural -> transposed window: lane 16q + j reads natural lane 4j + 3 - q
         uint32_t w = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((o - 1u) << 2), (int)win);
-        uint32_t* rec = fastRec[wave];
         const uint32_t rowBias = q << 6;
+        // four lengths per lane (lane t: positions hi - t .. hi - t - 3), one readlane per batch
+        const uint32_t pk = myL | (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 1u) << 2), (int)myL) << 8 |
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 2u) << 2), (int)myL) << 16 |
+                            (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane + 3u) << 2), (int)myL) << 24;
+        uint32_t kRec = 0;  // lane 16 r + j: the key of position i0 - r of the j-th batch before the last
         auto batch = [&](uint32_t t) {
+          const uint32_t P = rdlane(pk, t);
           uint32_t kv[4];
 #pragma unroll
           for (int r = 0; r < 4; r++) {
-            const int32_t Lr = (int32_t)rdlane(myL, t + (uint32_t)r);
+            const int32_t Lr = (int32_t)((P >> (8 * r)) & 0xFFu);
             kv[r] = (int32_t)o <= Lr - r ? w + kP[r] : kKeyNone;
           }
           // fold: rows 0, 1 of X = position 0, rows 2, 3 = position 2; Y likewise positions 1, 3
@@ -4331,10 +4371,7 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
           pm = min(pm, dpp_rows<kRowBcast31, 0xC>(0xFFFFFFFFu, pm));
           const uint32_t cp = min(pm, costNext + 1u);     // c_r - r
           const uint64_t use = __ballot(cp == a) & 0x0001000100010001ull;
-          if ((lane & 15u) == 0) {
-            rec[t + q] = key;
-            rec[64 + t + q] = cp;
-          }
+          kRec = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)kRec, kRowShr + 1, 0xF, 0xF, false);
           costNext = rdlane(cp, 48) + 3u;
           if (use) {
             lits = 3u - ((63u - (uint32_t)__builtin_clzll(use)) >> 4);
@@ -4355,13 +4392,14 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
         tFast = t;
         // transposed -> natural: lane l = cost[i0 + 1 + l] is transposed lane 16 (3 - (l & 3)) + (l >> 2)
         win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (3u - (lane & 3u))) + (lane >> 2)) << 2), (int)w);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t rk = rec[lane], rc = rec[64 + lane];
+        // position hi - l (l < tFast): its cost is in the window at offset tFast - l, its key in kRec
+        const uint32_t oc = tFast - lane - 1u;
+        const uint32_t rc = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (3u - (oc & 3u))) + ((oc >> 2) & 15u)) << 2), (int)w);
+        const uint32_t jb = (tFast >> 2) - 1u - (lane >> 2);
+        const uint32_t rk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (lane & 3u)) + (jb & 15u)) << 2), (int)kRec);
         if (lane < tFast) {
           kvBuf = rk + ((lane & 3u) << 6);
-          mcBuf = rc + (lane & 3u);
+          mcBuf = rc >> 6;
         }
         chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
       }
