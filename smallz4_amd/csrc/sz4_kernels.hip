@@ -4246,6 +4246,8 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
   auto key_cost = [&](int32_t, uint32_t key) -> uint32_t { return key >> 8; };
   RunEnd chain;
   bool noMatch = true;  // no position of the segment has a match: k_dp_fix repairs it in closed form
+  int32_t runE = -1;    // the last same-letter run end read, and its cost
+  uint32_t runC = 0;
 
   for (int32_t hi = segHi; hi >= segLo; hi -= 64) {
     const int32_t lo = hi - 63 > segLo ? hi - 63 : segLo;
@@ -4281,7 +4283,11 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
       // a same-letter run: every position takes its distance-1 match unconditionally (smallz4.h:413-419)
       const int32_t i = hi - (int32_t)lane;
       const int32_t E0 = hi + (int32_t)rdlane(myL, 0);
-      const uint32_t cE = E0 > segHi ? 0u : (E0 - hi < kRing - 64 ? ring[E0 & (kRing - 1)] : ld_fresh(&cost[E0]));
+      if (E0 != runE) {  // every chunk of a run shares its end: one load per run
+        runE = E0;
+        runC = E0 > segHi ? 0u : (E0 - hi < kRing - 64 ? ring[E0 & (kRing - 1)] : ld_fresh(&cost[E0]));
+      }
+      const uint32_t cE = runC;
       mcBuf = cE + 4u + (myL - 19u) / 255u;
       kvBuf = 0;
       bestBuf = myL;
@@ -4811,33 +4817,44 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     RunEnd chain;
     uint32_t closedCost = 0;  // closed-form chunk: cost at its end closedE
     int32_t closedE = 0;
+    int32_t runE = -1;        // the last same-letter run end read, and its exact cost
+    uint32_t runC = 0;
     bool done = false;
     int32_t maxReach = hi + 64;  // k_dp_fix<true>: highest position read above the segment
     int32_t lowW = hi;           // k_dp_fix<true>: lowest position written
     // the chunk's inputs are loaded one chunk ahead (positions below are not rewritten before)
-    uint32_t nL, nD, nS, nC, nR;
-    auto load_chunk = [&](int32_t h) {
+    // two chunks ahead: a block's repair is one wavefront per SIMD, nothing else hides the latency
+    uint32_t nL, nD, nS, nC, nR, mL, mD, mS, mC, mR;
+    auto load_chunk = [&](int32_t h, uint32_t& xL, uint32_t& xD, uint32_t& xS, uint32_t& xC, uint32_t& xR) {
       const int32_t ip = h - (int32_t)lane;
       const bool in = ip >= lo;
-      nL = in ? L[ip] : 0u;
-      nD = in ? (uint32_t)D[ip] : 0u;
-      nS = in ? S[ip] : 0u;
-      nC = in ? cost[ip] : 0u;
-      nR = in ? R[ip] : 0u;
+      xL = in ? L[ip] : 0u;
+      xD = in ? (uint32_t)D[ip] : 0u;
+      xS = in ? S[ip] : 0u;
+      xC = in ? cost[ip] : 0u;
+      xR = in ? R[ip] : 0u;
     };
-    nL = nD = nS = nC = nR = 0u;
-    if (!noMatch) load_chunk(hi);
+    nL = nD = nS = nC = nR = mL = mD = mS = mC = mR = 0u;
+    if (!noMatch) {
+      load_chunk(hi, nL, nD, nS, nC, nR);
+      if (hi - 64 >= lo) load_chunk(hi - 64, mL, mD, mS, mC, mR);
+    }
     for (int32_t h = hi; h >= lo && !done; h -= 64) {
       const int32_t ip = h - (int32_t)lane;
       const bool in = ip >= lo;
       uint32_t cL, cD, cS, cC, cR;
-      // opaque copies: the loop below must not wait for the prefetch issued right after
+      // opaque copies: the loop below must not wait for the prefetches issued right after
       asm volatile("v_mov_b32 %0, %1" : "=v"(cL) : "v"(nL));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cD) : "v"(nD));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cS) : "v"(nS));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cC) : "v"(nC));
       asm volatile("v_mov_b32 %0, %1" : "=v"(cR) : "v"(nR));
-      if (h - 64 >= lo && !noMatch) load_chunk(h - 64);
+      nL = mL;
+      nD = mD;
+      nS = mS;
+      nC = mC;
+      nR = mR;
+      if (h - 128 >= lo && !noMatch) load_chunk(h - 128, mL, mD, mS, mC, mR);
       const int32_t cl = h - 63 > lo ? h - 63 : lo;
       const uint32_t cnt = (uint32_t)(h - cl + 1);
       if constexpr (kPar) {
@@ -4885,7 +4902,12 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                    // extra(x + 1) <= extra(x) + 1)
                    const int32_t E0 = h + (int32_t)rdlane(cL, 0);
                    if (__ballot(in && !(cL >= kSameLetter && cD == 1u && ip + (int32_t)cL == E0)) == 0) {
-                     closedCost = cost_at(h, E0);
+                     // every chunk of a run shares its end: one (dependent, uncached) load per run
+                     if (E0 != runE) {
+                       runC = cost_at(h, E0);
+                       runE = E0;
+                     }
+                     closedCost = runC;
                      closedE = E0;
                      return true;
                    }
