@@ -270,6 +270,180 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
   return w;
 }
 
+#ifndef SZ4_UNLZ4_VEC
+#define SZ4_UNLZ4_VEC 1  // 0: k_unlz4_sizes walks the token chain one sequence at a time (A/B)
+#endif
+
+// every lane receives the sum of its 16-lane row
+__device__ __forceinline__ uint32_t un_row_sum(uint32_t v)
+{
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return v;
+}
+
+// unlz4_walk over a whole block (k_unlz4_sizes) with the token chain followed 64 window positions at a
+// time on the vector unit: lane l takes the pre-decoded header at window position 64 s + l, steps to
+// l + 3 + literals (+ 1 for a match-length byte) -- F1, 64 = out of the sub-window, or 64 where the
+// header needs the byte-wise path --, F2 .. F32 by doubling (ds_bpermute), and every lane finds the last
+// token start at or below itself by binary lifting from the entry.  The lanes that find themselves are
+// the block's sequences in this sub-window: stored by mbcnt rank, their decoded bytes summed by a row
+// reduction.  Whatever the pre-decoded headers do not cover goes through the same byte-wise sequence
+// as unlz4_walk, so the two agree on every frame, malformed ones included.
+__device__ uint64_t unlz4_walk_vec(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane,
+                                   uint4* __restrict__ seq, uint32_t cap, WalkEnd& W)
+{
+  W = WalkEnd{0u, 0u, 0u, 0u};
+  if (B.stored) {
+    W.exit = B.len;
+    W.end = 1;
+    return B.len;
+  }
+  const uint64_t end = B.src + B.len;
+  uint64_t r = B.src, w = 0;
+  uint32_t ns = 0;
+  auto push = [&](uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel) {
+    if (lane == 0) seq[ns] = make_uint4(lits, ml, off, frel);
+    ns++;
+  };
+  Window win{f, n, 0, 0};
+  auto one_seq = [&]() -> int {
+    const uint32_t tok = win.byte(r++, lane);
+    uint64_t lits = tok >> 4;
+    if (lits == 15) {
+      uint32_t x;
+      do {
+        if (r >= end) return 2;
+        x = win.byte(r++, lane);
+        lits += x;
+      } while (x == 255);
+    }
+    if (r + lits > end) return 2;
+    const uint32_t frel = (uint32_t)(r - B.src);
+    w += lits;
+    r += lits;
+    if (r == end) {  // the last sequence has literals only
+      push((uint32_t)lits, 0u, 0u, frel);
+      return 1;
+    }
+    if (r + 2 > end) return 2;
+    const uint32_t off = win.byte(r, lane) | (win.byte(r + 1, lane) << 8);
+    r += 2;
+    if (off == 0) return 2;  // "invalid offset" (smallz4cat.c:265-267)
+    uint64_t ml = kMinMatch + (tok & 15);
+    if (ml == kMinMatch + 15) {
+      uint32_t x;
+      do {
+        if (r >= end) return 2;
+        x = win.byte(r++, lane);
+        ml += x;
+      } while (x == 255);
+    }
+    push((uint32_t)lits, (uint32_t)ml, off, frel);
+    w += ml;
+    return 0;
+  };
+  const uint32_t fastEnd = B.len > 20u ? B.len - 20u : 0u;
+  while (r < end) {
+    win.fill(r, lane);
+    uint32_t cand[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t tok = (win.w >> (8 * k)) & 0xFFu;
+      const uint32_t a = 4u * lane + (uint32_t)k + 1u + (tok >> 4);  // window index of the offset
+      const uint32_t ia = (a >> 2) << 2;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)ia, (int)win.w);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ia + 4u), (int)win.w);
+      const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (a & 3u)));
+      const bool ext = (tok & 15u) == 15u;
+      const uint32_t last = a + 1u + (ext ? 1u : 0u);  // last window byte the header reads
+      const bool ok = (tok >> 4) != 15u && last < 256u && !(ext && ((v >> 16) & 0xFFu) == 255u) && (v & 0xFFFFu) != 0u;
+      cand[k] = ok ? (tok | (v << 8)) : 0xFFFFFFFFu;  // v's bytes 0-2: offset, extension byte
+    }
+    const uint32_t wb = (uint32_t)(win.base - B.src);  // window base, block-relative
+    uint32_t rr = (uint32_t)(r - B.src);
+    bool slow = false, bad = false;
+    while (rr < fastEnd) {
+      const uint32_t q0 = rr - wb;
+      if (q0 >= 192u) break;  // refill
+      const uint32_t sb = q0 & ~63u, e = q0 & 63u;
+      const int src = (int)(((sb >> 2) + (lane >> 2)) << 2);
+      const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[0]);
+      const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[1]);
+      const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[2]);
+      const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[3]);
+      const uint32_t c = (lane & 2u) ? ((lane & 1u) ? g3 : g2) : ((lane & 1u) ? g1 : g0);
+      const uint32_t pos = wb + sb + lane;  // block-relative frame offset of this lane's token
+      const bool ok = c != 0xFFFFFFFFu && pos < fastEnd;
+      const uint32_t lits = (c >> 4) & 15u, nib = c & 15u;
+      const uint32_t step = 3u + lits + (nib == 15u ? 1u : 0u);
+      uint32_t F[6];
+      F[0] = ok && lane + step < 64u ? lane + step : 64u;
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(F[k - 1] << 2), (int)F[k - 1]);
+        F[k] = F[k - 1] >= 64u ? 64u : g;
+      }
+      uint32_t x = e;
+      {
+        const uint32_t y = un_rdlane(F[5], e);
+        x = y <= lane ? y : x;
+      }
+#pragma unroll
+      for (int k = 4; k >= 0; k--) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)F[k]);
+        x = y <= lane ? y : x;
+      }
+      const bool tok = x == lane && ok;
+      const uint64_t tb = __ballot(tok);
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(tb);
+      if (ns + cnt > cap) {  // cannot happen in a well-formed block
+        bad = true;
+        break;
+      }
+      const uint32_t ml = kMinMatch + nib + (nib == 15u ? c >> 24 : 0u);
+      if (tok) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(tb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb, 0u));
+        seq[ns + rank] = make_uint4(lits, ml, (c >> 8) & 0xFFFFu, pos + 1u);
+      }
+      ns += cnt;
+      const uint32_t rs = un_row_sum(tok ? lits + ml : 0u);
+      w += (uint64_t)(un_rdlane(rs, 0) + un_rdlane(rs, 16) + un_rdlane(rs, 32) + un_rdlane(rs, 48));
+      const uint32_t p = un_rdlane(x, 63);  // the last token start of the path in this sub-window
+      if (!((__ballot(ok) >> p) & 1ull)) {
+        // a header the window did not pre-decode: from a refilled window, or byte-wise at the window start
+        rr = wb + sb + p;
+        slow = sb + p < 64u;
+        break;
+      }
+      rr = wb + sb + p + un_rdlane(step, p);
+    }
+    if (bad) {
+      W.exit = rr;
+      return kNone;
+    }
+    r = B.src + rr;
+    if (rr < fastEnd && !slow) continue;  // refill
+    if (r >= end) break;
+    if (ns >= cap) {
+      W.exit = rr;
+      return kNone;
+    }
+    const int e = one_seq();
+    if (e == 2) {
+      W.exit = (uint32_t)(r - B.src);
+      return kNone;
+    }
+    if (e == 1) break;
+  }
+  W.exit = (uint32_t)(r - B.src);
+  W.ns = ns;
+  W.end = r >= end ? 1u : 0u;
+  return w;
+}
+
 // Replays block bi's sequence list into `out` (and the ring); returns the decoded length.
 __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t bi, uint32_t lane,
                                  const uint4* __restrict__ seq, uint8_t* __restrict__ out, uint8_t* __restrict__ ring,
@@ -472,7 +646,11 @@ __global__ __launch_bounds__(64) void k_unlz4_sizes(const uint8_t* __restrict__ 
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
   WalkEnd W;
+#if SZ4_UNLZ4_VEC
+  const uint64_t size = unlz4_walk_vec(f, n, B, lane, seq_base(seqAll, B, bi), seq_cap(B), W);
+#else
   const uint64_t size = unlz4_walk<false, false>(f, n, B, lane, 0u, B.len, seq_base(seqAll, B, bi), seq_cap(B), nullptr, 0u, W);
+#endif
   if (lane == 0) {
     blk[bi].size = size;
     blk[bi].nseq = W.ns;
