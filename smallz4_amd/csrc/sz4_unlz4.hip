@@ -445,10 +445,13 @@ __device__ uint64_t unlz4_walk_vec(const uint8_t* __restrict__ f, uint64_t n, co
 }
 
 // Replays block bi's sequence list into `out` (and the ring); returns the decoded length.
+// From sequence b0Start on, with wStart bytes of the block already decoded (and drained): how the vector
+// decoder below hands a block over when a match reads below the block start.
 __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t bi, uint32_t lane,
                                  const uint4* __restrict__ seq, uint8_t* __restrict__ out, uint8_t* __restrict__ ring,
                                  const uint8_t* __restrict__ dict, uint64_t dl, const UnBlock* __restrict__ blk,
-                                 uint32_t* __restrict__ done, uint32_t* __restrict__ status)
+                                 uint32_t* __restrict__ done, uint32_t* __restrict__ status, uint32_t b0Start = 0,
+                                 uint64_t wStart = 0)
 {
   if (B.stored) {
     // later blocks read it from `out`
@@ -457,9 +460,9 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
   }
   uint64_t floorPos = B.dst;  // output below this is read only after its blocks are done
   uint32_t waitIdx = bi;
-  uint64_t w = 0;             // bytes decoded so far
-  uint64_t synced = B.dst;    // this block's output below it is drained and readable from `out`
-  for (uint32_t b0 = 0; b0 < B.nseq; b0 += 64) {
+  uint64_t w = wStart;             // bytes decoded so far
+  uint64_t synced = B.dst + wStart;  // this block's output below it is drained and readable from `out`
+  for (uint32_t b0 = b0Start; b0 < B.nseq; b0 += 64) {
     const uint32_t cnt = B.nseq - b0 < 64u ? B.nseq - b0 : 64u;
     const uint4 q = lane < cnt ? seq[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
     // output offset of every sequence's literals (a wavefront scan of literals + match length)
@@ -563,6 +566,115 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
       }
     }
     w += un_rdlane(incl, cnt - 1u);
+  }
+  return w;
+}
+
+#ifndef SZ4_UNLZ4_DEC_VEC
+#define SZ4_UNLZ4_DEC_VEC 1  // 0: k_unlz4_blocks replays one sequence at a time (A/B)
+#endif
+
+// inclusive max-scan over the 64 lanes (rows by DPP shifts, then the row broadcasts)
+__device__ __forceinline__ uint32_t un_scan_max(uint32_t v)
+{
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));  // row_shr:1
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));  // row_shr:2
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));  // row_shr:4
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));  // row_shr:8
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
+}
+
+// Block bi's sequence list replayed 64 OUTPUT bytes per step instead of one sequence per step: for an
+// output window [W, W + 64) the sequences starting in it mark their first byte (an LDS slot per byte),
+// a max-scan gives every lane its sequence, four ds_bpermutes its fields; a literal byte comes from the
+// frame, a match byte from `out` / the LDS ring when its source lies before the window, and from an
+// earlier lane of the window otherwise (resolved by pointer jumping: src -> src - offset until a known
+// byte, at most log2(64) rounds per distinct offset).  Blocks whose matches stay inside the block
+// (independent blocks: every frame bench.py decodes); the first batch with a match reaching below the
+// block start (linked blocks, a dictionary) or an empty sequence continues in unlz4_decode.
+__device__ uint64_t unlz4_decode_vec(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t bi,
+                                     uint32_t lane, const uint4* __restrict__ seq, uint8_t* __restrict__ out,
+                                     uint8_t* __restrict__ ring, uint32_t* __restrict__ slot,
+                                     const uint8_t* __restrict__ dict, uint64_t dl, const UnBlock* __restrict__ blk,
+                                     uint32_t* __restrict__ done, uint32_t* __restrict__ status)
+{
+  if (B.stored) {
+    for (uint64_t k = lane; k < B.len; k += 64) out[B.dst + k] = f[B.src + k];
+    return B.len;
+  }
+  uint64_t w = 0;            // block-relative output of the batches done
+  uint64_t synced = 0;       // block-relative: output below it is drained and readable from `out`
+  slot[lane] = 0;
+  for (uint32_t b0 = 0; b0 < B.nseq; b0 += 64) {
+    const uint32_t cnt = B.nseq - b0 < 64u ? B.nseq - b0 : 64u;
+    const uint4 q = lane < cnt ? seq[b0 + lane] : make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t tot = q.x + q.y;
+    const uint32_t incl = un_incl_scan_add(tot, lane);
+    const uint32_t pj = incl - tot;  // batch-relative output offset of sequence `lane`
+    const uint32_t blen = un_rdlane(incl, cnt - 1u);
+    // a match reading below the block start, or a sequence of no bytes: the sequence-wise decoder
+    const bool far = lane < cnt && q.y != 0u && w + pj + q.x < (uint64_t)q.z;
+    if (__ballot(far || (lane < cnt && tot == 0u))) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+      return unlz4_decode(f, n, B, bi, lane, seq, out, ring, dict, dl, blk, done, status, b0, w);
+    }
+    uint32_t jc = 0;  // 1 + the sequence covering the byte before the window
+    for (uint32_t W = 0; W < blen; W += 64) {
+      const uint64_t cur = w + W;  // block-relative first byte of the window
+      if (cur - synced >= kSync) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        synced = cur;
+      }
+      if (lane < cnt && pj >= W && pj - W < 64u) slot[pj - W] = lane + 1u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t mark = slot[lane];
+      slot[lane] = 0;
+      const uint32_t sc = un_scan_max(mark);
+      const uint32_t jj = (sc ? sc : jc) - 1u;  // this lane's sequence
+      jc = un_rdlane(sc ? sc : jc, 63);
+      const uint32_t o = W + lane;  // batch-relative output byte
+      const bool valid = o < blen;
+      const int addr = (int)(jj << 2);
+      const uint32_t P = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)pj);
+      const uint32_t L = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)q.x);
+      const uint32_t off = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)q.z);
+      const uint32_t fr = (uint32_t)__builtin_amdgcn_ds_bpermute(addr, (int)q.w);
+      const uint32_t k = o - P;
+      const bool lit = k < L;
+      const uint64_t ob = w + o;    // block-relative
+      const uint64_t src = ob - off;  // a match's source (>= 0: checked per batch)
+      const bool inWin = valid && !lit && src >= cur;
+      uint32_t val = 0;
+      if (valid && lit) val = f[B.src + fr + k];
+      // the ring holds [cur - kRing, cur) until this window's stores; further back is drained in `out`
+      else if (valid && !inWin) val = src + kRing >= cur ? ring[(B.dst + src) & (kRing - 1u)] : out[B.dst + src];
+      bool known = !inWin;
+      uint32_t ref = inWin ? (uint32_t)(src - cur) : lane;
+      while (__ballot(!known)) {
+        const uint32_t kv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ref << 2), known ? 1 : 0);
+        const uint32_t vv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ref << 2), (int)val);
+        const uint32_t rv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ref << 2), (int)ref);
+        if (!known) {
+          if (kv) {
+            val = vv;
+            known = true;
+          } else {
+            ref = rv;
+          }
+        }
+      }
+      if (valid) {
+        out[B.dst + ob] = (uint8_t)val;
+        ring[(B.dst + ob) & (kRing - 1u)] = (uint8_t)val;
+      }
+    }
+    w += blen;
   }
   return w;
 }
@@ -673,8 +785,14 @@ __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__
   const uint32_t bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
+#if SZ4_UNLZ4_DEC_VEC
+  __shared__ uint32_t slot[64];
+  const uint64_t got = unlz4_decode_vec(f, n, B, bi, lane, seq_base(const_cast<uint4*>(seqAll), B, bi), out, ring, slot,
+                                        dict, dl, blk, done, status);
+#else
   const uint64_t got = unlz4_decode(f, n, B, bi, lane, seq_base(const_cast<uint4*>(seqAll), B, bi), out, ring, dict, dl, blk,
                                     done, status);
+#endif
   if (lane == 0 && got != B.size) atomicOr(status, 1u);
   // publish: this wave's stores drained, written back (agent release), then the flag
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
