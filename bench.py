@@ -288,6 +288,26 @@ def pmc_traffic(cfg):
     return best
 
 
+def valu_ceiling():
+    """(source, VALU instructions per SIMD per cycle at CLOCK_GHZ) sustained by tools/valu_ceiling.hip
+    (independent v_add/v_xor chains, 32 waves per CU) on the MI355X, from profiles/valu_ceiling_*.json."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "valu_ceiling_*.json")))
+    if not paths:
+        return None
+    best = 0.0
+    with open(paths[-1]) as f:
+        for line in f:
+            try:
+                rec = json.loads(line)
+            except ValueError:
+                continue
+            if rec.get("variant") == "add_xor":
+                best = max(best, rec["valu_instr_per_s"])
+    if not best:
+        return None
+    return os.path.relpath(paths[-1], ROOT), round(best / 1024 / (CLOCK_GHZ * 1e9), 4)
+
+
 def spawn_ranks(args):
     """`--gpus N` outside torch.distributed: run N ranks through torch.distributed.run as a child
     process (this process has not touched the GPU) and return its exit status."""
@@ -631,6 +651,12 @@ def main():
             if rec_p.get("valu_per_simd_cycle") is not None:
                 issue.update({"valu_per_simd_cycle": rec_p["valu_per_simd_cycle"], "valu_peak": 0.5,
                               "valu_frac": round(rec_p["valu_per_simd_cycle"] / 0.5, 4)})
+                ceil = valu_ceiling()
+                if ceil:
+                    # the integer VALU rate the chip sustains (tools/valu_ceiling.hip), in the same units
+                    issue.update({"valu_ceiling_measured": ceil[1],
+                                  "valu_frac_of_measured": round(rec_p["valu_per_simd_cycle"] / ceil[1], 4),
+                                  "valu_ceiling_source": ceil[0]})
             if rec_p.get("salu_per_cu_cycle") is not None:
                 issue.update({"salu_per_cu_cycle": rec_p["salu_per_cu_cycle"], "salu_peak": 1.0,
                               "salu_frac": round(rec_p["salu_per_cu_cycle"], 4)})
