@@ -419,6 +419,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 
 // k_sort's shared memory (57 KB).  When k_find_sorted sorts its own segment it lives in the window
 // buffer, which is loaded only after the sort.
+#ifndef SZ4_DP_BUMP
+#define SZ4_DP_BUMP 1  // 0: a fast chunk with a reachable literal-length bump finishes in the general loop
+#endif
 #ifndef SZ4_DP_VEC
 #define SZ4_DP_VEC 1  // 0: the parse's fast batches one position at a time in the scalar unit (A/B)
 #endif
@@ -4215,9 +4218,14 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
   if (G.k > 0) {
     uint32_t* R = reach + base;
     uint32_t carry = 0;
+    // lengths one chunk ahead (opaque copy: the scan must not wait for the next load)
+    uint32_t nxt = segLo + (int32_t)lane <= segHi ? L[segLo + (int32_t)lane] : 0u;
     for (int32_t c0 = segLo; c0 <= segHi; c0 += 64) {
       const int32_t q = c0 + (int32_t)lane;
-      const uint32_t v = q <= segHi ? (uint32_t)q + L[q] : 0u;
+      uint32_t Lq;
+      asm volatile("v_mov_b32 %0, %1" : "=v"(Lq) : "v"(nxt));
+      nxt = q + 64 <= segHi ? L[q + 64] : 0u;
+      const uint32_t v = q <= segHi ? (uint32_t)q + Lq : 0u;
       const uint32_t incl = wave_incl_scan_max(v);
       uint32_t excl = __shfl_up(incl, 1, 64);
       excl = lane == 0 ? carry : (excl > carry ? excl : carry);
@@ -4395,6 +4403,41 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
           t = tb + 4u;
           if (tb + 4u < 64u && lits + 4u >= litBump) break;
         }
+#if SZ4_DP_BUMP
+        // the rest of the chunk with a literal-length bump reachable: the literal term of the prefix minimum
+        // costs one more from the position whose run length reaches litBump on (only the all-literal path
+        // from the batch start can reach it: after a match the run restarts below 4 < 15)
+        for (; t < 64u; t += 4u) {
+          const uint32_t P = rdlane(pk, t);
+          uint32_t kv[4];
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int32_t Lr = (int32_t)((P >> (8 * r)) & 0xFFu);
+            kv[r] = (int32_t)o <= Lr - r ? w + kP[r] : kKeyNone;
+          }
+          auto x = __builtin_amdgcn_permlane32_swap(kv[0], kv[2], false, false);
+          auto y = __builtin_amdgcn_permlane32_swap(kv[1], kv[3], false, false);
+          const uint32_t X = min(x[0], x[1]), Y = min(y[0], y[1]);
+          auto z = __builtin_amdgcn_permlane16_swap(X, Y, false, false);
+          const uint32_t key = row_min(min(z[0], z[1]));
+          const uint32_t a = key >> 6;
+          uint32_t pm = min(a, dpp_rows<kRowBcast15, 0xA>(0xFFFFFFFFu, a));
+          pm = min(pm, dpp_rows<kRowBcast31, 0xC>(0xFFFFFFFFu, pm));
+          const uint32_t rStar = litBump - lits - 1u;  // the position whose literal is the bumped one
+          const uint32_t cp = min(pm, costNext + 1u + (q >= rStar ? 1u : 0u));
+          const uint64_t use = __ballot(cp == a) & 0x0001000100010001ull;
+          kRec = (uint32_t)__builtin_amdgcn_update_dpp((int)key, (int)kRec, kRowShr + 1, 0xF, 0xF, false);
+          costNext = rdlane(cp, 48) + 3u;
+          if (use) {
+            lits = 3u - ((63u - (uint32_t)__builtin_clzll(use)) >> 4);
+            litBump = 15u;
+          } else {
+            lits += 4u;
+            if (rStar < 4u) litBump += 255u;
+          }
+          w = (uint32_t)__builtin_amdgcn_update_dpp((int)((cp << 6) + rowBias), (int)w, kRowShr + 1, 0xF, 0xF, false);
+        }
+#endif
         tFast = t;
         // transposed -> natural: lane l = cost[i0 + 1 + l] is transposed lane 16 (3 - (l & 3)) + (l >> 2)
         win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (3u - (lane & 3u))) + (lane >> 2)) << 2), (int)w);
@@ -5511,18 +5554,28 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_seg_tokens(const Block* __re
   const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kWalkCap);
   Token* tok = tokAll + B.tokOff + inf.x;
   uint32_t carryEnd = inf.y, bytes = 0;
+  // loads run ahead: the next batch's match positions, then their lengths and distances
+  uint32_t pN = lane < m ? slots[st.x + lane] : 0u;
+  uint32_t LN = lane < m ? L[pN] : 0u, DN = lane < m ? (uint32_t)D[pN] : 0u;
+  uint32_t pNN = 64u + lane < m ? slots[st.x + 64u + lane] : 0u;
   for (uint32_t c0 = 0; c0 < m; c0 += 64) {
     const uint32_t t = c0 + lane;
     const bool valid = t < m;
-    const uint32_t p = valid ? slots[st.x + t] : 0u;
-    const uint32_t Lm = valid ? L[p] : 0u;
+    uint32_t p, Lm, Dm;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(p) : "v"(pN));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(Lm) : "v"(LN));
+    asm volatile("v_mov_b32 %0, %1" : "=v"(Dm) : "v"(DN));
+    pN = pNN;
+    LN = t + 64u < m ? L[pN] : 0u;
+    DN = t + 64u < m ? (uint32_t)D[pN] : 0u;
+    pNN = t + 128u < m ? slots[st.x + t + 128u] : 0u;
     const uint32_t end = p + Lm;
     uint32_t prev = __shfl_up(end, 1, 64);
     if (lane == 0) prev = carryEnd;
     uint32_t sz = 0;
     if (valid) {
       const uint32_t lits = p - prev;
-      tok[t] = Token{lits ? prev : 0u, lits, Lm, (uint32_t)D[p]};
+      tok[t] = Token{lits ? prev : 0u, lits, Lm, Dm};
       sz = (uint32_t)token_bytes(lits, Lm, false);
     }
     bytes += wave_sum_u32(sz);
@@ -5654,7 +5707,25 @@ __global__ __launch_bounds__(64 * kSegWaves) void k_write_seg(const uint8_t* __r
         *o++ = (uint8_t)v;
       }
       if (lits <= kOwnLits) {
-        for (uint64_t k = 0; k < lits; k++) o[k] = src[T.litFrom + k];
+        // 8 bytes per round: three aligned dwords loaded together, then byte stores (one load latency
+        // per 8 literals instead of one per literal)
+        // (the three dwords lie inside the block, the input buffer's alignment taken into account)
+        for (uint32_t k = 0; k < (uint32_t)lits; k += 8) {
+          const uint64_t a = (uint64_t)T.litFrom + k;
+          const uint32_t nk = (uint32_t)lits - k < 8u ? (uint32_t)lits - k : 8u;
+          const uintptr_t ab = reinterpret_cast<uintptr_t>(src + a);
+          if (a >= 4u && a + 12u <= n) {
+            const uint32_t* wp = reinterpret_cast<const uint32_t*>(ab & ~(uintptr_t)3);
+            const uint32_t w0 = wp[0], w1 = wp[1], w2 = wp[2];
+            const uint32_t sh = (uint32_t)(ab & 3u);
+            const uint32_t v0 = __builtin_amdgcn_alignbyte(w1, w0, sh), v1 = __builtin_amdgcn_alignbyte(w2, w1, sh);
+#pragma unroll
+            for (uint32_t b = 0; b < 8; b++)
+              if (b < nk) o[k + b] = (uint8_t)((b < 4 ? v0 : v1) >> (8 * (b & 3)));
+          } else {
+            for (uint32_t b = 0; b < nk; b++) o[k + b] = src[a + b];
+          }
+        }
       } else {
         isLong = true;  // copied by the whole wavefront below
         s_ld[wave][lane] = (uint32_t)(o - dst);
