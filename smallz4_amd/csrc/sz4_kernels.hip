@@ -427,6 +427,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 #endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
+#ifndef SZ4_RUN_PREFIX
+#define SZ4_RUN_PREFIX 1  // 0: k_find extends candidates inside a same-letter run byte by byte (A/B)
+#endif
 #ifndef SZ4_HIT2
 #define SZ4_HIT2 1  // 0: round 3's filter-hit code (masks from need bytes, satOk applied afterwards)
 #endif
@@ -809,6 +812,21 @@ __device__ __forceinline__ uint32_t prefix_if_at_least(const Src& src, uint64_t 
     k += 4;
   }
   return k < room ? k : room;
+}
+
+// prefix_if_at_least with a same-letter run [rLo, rHi) known around p (rHi capped at the block's last
+// searchable byte): a candidate inside the run matches exactly up to the run's end, so no byte loop
+// (O(1) instead of O(run) per candidate: greedy/lazy levels on long runs were quadratic)
+template <class Src>
+__device__ __forceinline__ uint32_t prefix_run(const Src& src, uint64_t p, uint64_t c, uint32_t need, uint32_t room,
+                                               uint64_t rLo, uint64_t rHi)
+{
+  if (p >= rLo && p < rHi && c >= rLo) {
+    const uint64_t e = rHi - p;
+    const uint32_t pr = e < (uint64_t)room ? (uint32_t)e : room;
+    return pr >= need ? pr : 0u;
+  }
+  return prefix_if_at_least(src, p, c, need, room);
 }
 
 // ================================================================================================
@@ -1790,6 +1808,34 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     int64_t slot = 0;
     uint32_t carryLen = 0, carryDist = 0;
     uint32_t resLen = pass1Len, resDist = pass1Dist;  // lane rowBase+t holds the result of target first+rowBase+t
+    uint64_t runLo = 0, runHi = 0;  // the row's last same-letter run (SZ4_RUN_PREFIX)
+    bool wantRun = false;
+    int64_t runJump = -1;            // the highest slot of the row's group below runLo, for (jumpLo, jumpGs)
+    uint64_t jumpLo = ~0ull;
+    uint32_t jumpGs = 0;
+    // after a target's first step inside a run, the rest of the group's candidates inside the run match
+    // exactly as far as the nearest one (the run's end): none can win, the walk jumps below the run
+    auto run_jump = [&]() {
+      if (!(SZ4_RUN_PREFIX && p >= runLo && p < runHi && slot >= (int64_t)gsCur)) return;
+      if (S.w0 + slot_pos(compact, small, (uint32_t)slot) < runLo) return;
+      if (jumpLo != runLo || jumpGs != gsCur) {
+        int64_t a = (int64_t)gsCur, b = slot;  // largest s in [a, b] with position < runLo, else a - 1
+        if (S.w0 + slot_pos(compact, small, (uint32_t)a) >= runLo) {
+          b = a - 1;
+        } else {
+          while (a < b) {
+            const int64_t mid = (a + b + 1) >> 1;
+            if (S.w0 + slot_pos(compact, small, (uint32_t)mid) < runLo) a = mid;
+            else b = mid - 1;
+          }
+          b = a;
+        }
+        runJump = b;
+        jumpLo = runLo;
+        jumpGs = gsCur;
+      }
+      if (runJump < slot) slot = runJump;
+    };
 
     while (true) {
       const bool live = j < rowCnt;
@@ -1820,6 +1866,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
         } else if (!done) {
           key = src.ld4(p);
           room = (uint32_t)(stopAbs - p);
+          wantRun = SZ4_RUN_PREFIX && key == (key & 0xFFu) * 0x01010101u && !(p >= runLo && p < runHi);
           lb = p > kWindow ? p - kWindow : 0;
           if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
           slot = (int64_t)rCur - 1;
@@ -1865,6 +1912,58 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           }
         }
       }
+#if SZ4_RUN_PREFIX
+      // a target that starts four equal bytes outside the row's cached run: the run's extent, forward to
+      // the block's last searchable byte and backward to the window base, 64 bytes per step over the
+      // row's 16 lanes (once per run and row)
+      if (__ballot(wantRun)) {
+        const bool want = wantRun;
+        wantRun = false;
+        const uint32_t pat = (key & 0xFFu) * 0x01010101u;
+        bool go = want;
+        uint64_t hiF = p;
+        for (uint64_t k = 0; __ballot(go); k += 64) {
+          const uint64_t q = p + k + 4u * li;
+          const uint32_t x = go && q < stopAbs ? (src.ld4(q) ^ pat) : 0xFFFFFFFFu;
+          const uint32_t mis = (uint32_t)(__ballot(go && x != 0u) >> rowBase) & 0xFFFFu;
+          if (go && mis) {
+            const uint32_t f = (uint32_t)__builtin_ctz(mis);
+            const uint32_t xf = (uint32_t)__shfl(x, (int)(rowBase + f), 64);
+            hiF = p + k + 4u * f + ((uint32_t)__builtin_ctz(xf) >> 3);
+            go = false;
+          }
+        }
+        go = want;
+        uint64_t loF = p;
+        for (uint64_t k = 0; __ballot(go); k += 64) {
+          const int64_t q = (int64_t)p - (int64_t)k - 4 * (int64_t)(li + 1u);  // bytes q .. q + 3
+          uint32_t hm = 0;                                                     // 1 + highest mismatching byte
+          bool m = false;
+          if (go) {
+            if (q < (int64_t)S.w0) {
+              m = true;
+              hm = 4u;  // not in the window: the run is only known down to the word above it
+            } else {
+              const uint32_t x = src.ld4((uint64_t)q) ^ pat;
+              m = x != 0u;
+              hm = m ? (uint32_t)(31 - __builtin_clz(x)) / 8u + 1u : 0u;
+            }
+          }
+          const uint32_t mis = (uint32_t)(__ballot(go && m) >> rowBase) & 0xFFFFu;
+          if (go && mis) {
+            const uint32_t f = (uint32_t)__builtin_ctz(mis);  // nearest word below p with a mismatch
+            const int64_t qf = (int64_t)p - (int64_t)k - 4 * (int64_t)(f + 1u);
+            const uint32_t hf = (uint32_t)__shfl(hm, (int)(rowBase + f), 64);
+            loF = (uint64_t)(qf + (int64_t)hf);  // bytes [loF, p) verified equal (>= S.w0: see hm)
+            go = false;
+          }
+        }
+        if (want) {
+          runLo = loF;
+          runHi = hiF < stopAbs ? hiF : stopAbs;
+        }
+      }
+#endif
       // one step: 16 candidates of the row's key group, nearest first
       const bool act = live && !done;
       bool valid = false, exhausted = true;
@@ -1880,11 +1979,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
             if (unlimited) {
               if (dist != bestDist) {
                 const uint32_t need = dist < bestDist ? bestLen : bestLen + 1;
-                got = prefix_if_at_least(src, p, c, need < 4 ? 4 : need, room);
+                got = prefix_run(src, p, c, need < 4 ? 4 : need, room, runLo, runHi);
                 if (got < need) got = 0;
               }
             } else {
-              got = prefix_if_at_least(src, p, c, bestLen + 1 < 4 ? 4 : bestLen + 1, room);
+              got = prefix_run(src, p, c, bestLen + 1 < 4 ? 4 : bestLen + 1, room, runLo, runHi);
               if (got <= bestLen) got = 0;
             }
           }
@@ -1907,6 +2006,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           if (rowExhausted != 0u) done = true;                           // key group / window exhausted
           else if (bestLen >= room && farDist >= bestDist) done = true;   // nothing left can win
           slot -= 16;
+          if (!done) run_jump();
         }
       } else {
         // strict improvements in chain order ("records"); the reference stops after maxChain of them
@@ -1936,6 +2036,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
           }
           if (rowExhausted != 0u || bestLen >= room) done = true;
           slot -= 16;
+          if (!done) run_jump();
         }
       }
       if (live && done) {
