@@ -2214,6 +2214,71 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     __syncthreads();
   }
 
+  // same-letter runs (SZ4_RUN_PREFIX): the wave's last run [runLo, runHi) of a target's byte (runHi capped
+  // at the block's last searchable byte).  A candidate inside the target's run matches exactly up to the
+  // run's end, so after the nearest such candidate none of the others can win: the walk jumps below the
+  // run (the slot, cached per run and key group).  Without it a run makes the walk quadratic.
+  uint64_t runLo = 0, runHi = 0, jumpLo = ~0ull;
+  int32_t jumpSlot = -1, jumpGs = -1;
+  auto run_of = [&](uint64_t p, uint32_t key) {  // wave-uniform
+    if (!SZ4_RUN_PREFIX || key != (key & 0xFFu) * 0x01010101u || (p >= runLo && p < runHi)) return;
+    const uint32_t pat = key;
+    uint64_t hi = p;
+    for (uint64_t k = 0;; k += 256) {
+      const uint64_t q = p + k + 4u * lane;
+      const uint32_t x = q < stopAbs ? (src.ld4(q) ^ pat) : 0xFFFFFFFFu;
+      const uint64_t mis = __ballot(x != 0u);
+      if (mis) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(mis);
+        hi = p + k + 4u * f + ((uint32_t)__builtin_ctz(rdlane(x, f)) >> 3);
+        break;
+      }
+    }
+    uint64_t lo = p;
+    for (uint64_t k = 0;; k += 256) {
+      const int64_t q = (int64_t)p - (int64_t)k - 4 * (int64_t)(lane + 1u);
+      uint32_t hm = 4u;  // below the window: the run is only known down to the word above
+      bool m = true;
+      if (q >= (int64_t)S.w0) {
+        const uint32_t x = src.ld4((uint64_t)q) ^ pat;
+        m = x != 0u;
+        hm = m ? (uint32_t)(31 - __builtin_clz(x)) / 8u + 1u : 0u;
+      }
+      const uint64_t mis = __ballot(m);
+      if (mis) {
+        const uint32_t f = (uint32_t)__builtin_ctzll(mis);
+        lo = (uint64_t)((int64_t)p - (int64_t)k - 4 * (int64_t)(f + 1u) + (int64_t)rdlane(hm, f));
+        break;
+      }
+    }
+    runLo = lo;
+    runHi = hi < stopAbs ? hi : stopAbs;
+  };
+  auto run_prefix = [&](uint64_t p, uint64_t c, uint32_t room, bool& known) -> uint32_t {
+    known = SZ4_RUN_PREFIX && p >= runLo && p < runHi && c >= runLo;
+    const uint64_t e = runHi - p;
+    return e < (uint64_t)room ? (uint32_t)e : room;
+  };
+  // the highest slot of key group [gs, s] whose position is below runLo (gs - 1: none)
+  auto run_jump_slot = [&](int32_t gs, int32_t s) -> int32_t {
+    if (jumpLo == runLo && jumpGs == gs) return jumpSlot;
+    int32_t a = gs, b = s;
+    if (S.w0 + slot_pos(compact, small, (uint32_t)a) >= runLo) {
+      b = a - 1;
+    } else {
+      while (a < b) {
+        const int32_t mid = (a + b + 1) >> 1;
+        if (S.w0 + slot_pos(compact, small, (uint32_t)mid) < runLo) a = mid;
+        else b = mid - 1;
+      }
+      b = a;
+    }
+    jumpLo = runLo;
+    jumpGs = gs;
+    jumpSlot = b;
+    return b;
+  };
+
   // best match of target p (wave-uniform): carry (cLen, cDist), exact = the carry is p-1's maximum
   auto best_of = [&](uint64_t p, uint32_t cLen, uint32_t cDist, bool exact, uint32_t& bLen, uint32_t& bDist) {
 #if SZ4_DIAG == 5
@@ -2225,6 +2290,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
     uint32_t bestLen = 0, bestDist = 0;
     bool carryOk = false;
+    run_of(p, key);
     if (cDist != 0u && cLen >= 5u) {
       const uint64_t c = p - cDist;
       if (c >= lb && !excluded(c)) {
@@ -2245,7 +2311,9 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     // pass 1's nearest candidate at its cap
     const uint32_t seed = mdist[p - matchBase];
     if (seed != 0u && (bestLen < room || seed < bestDist)) {
-      const uint32_t l = wave_exact_prefix(src, p, p - seed, room);
+      bool rk;
+      const uint32_t rl = run_prefix(p, p - seed, room, rk);
+      const uint32_t l = rk ? rl : wave_exact_prefix(src, p, p - seed, room);
       if (l > bestLen || (l == bestLen && seed < bestDist)) {
         bestLen = l;
         bestDist = seed;
@@ -2257,9 +2325,29 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       // below rejects the others at a glance
       const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)s);
       if (c >= lb && src.ld4(c) == key) {
-        bestLen = wave_exact_prefix(src, p, c, room);
+        bool rk;
+        const uint32_t rl = run_prefix(p, c, room, rk);
+        bestLen = rk ? rl : wave_exact_prefix(src, p, c, room);
         bestDist = (uint32_t)(p - c);
         s--;
+      }
+    }
+    // inside a run: the nearest unvisited candidate, when it lies in the run, is the best of the run's
+    // candidates (all match up to the run's end; it is the nearest); the walk goes on below the run
+    if (SZ4_RUN_PREFIX && key == (key & 0xFFu) * 0x01010101u && p >= runLo && p < runHi && s >= gs) {
+      const uint64_t c0 = S.w0 + slot_pos(compact, small, (uint32_t)s);
+      if (c0 >= runLo) {
+        if (c0 >= lb) {
+          bool rk;
+          const uint32_t rl = run_prefix(p, c0, room, rk);
+          const uint32_t d0 = (uint32_t)(p - c0);
+          if (bestDist == 0u || rl > bestLen || (rl == bestLen && d0 < bestDist)) {
+            bestLen = rl;
+            bestDist = d0;
+          }
+        }
+        const int32_t js = run_jump_slot(gs, s);
+        if (js < s) s = js;
       }
     }
     while (s >= gs) {
