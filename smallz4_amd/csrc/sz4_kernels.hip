@@ -4032,34 +4032,37 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, con
   // blocks without shortcut intervals or runs beyond MaxSameLetter: k_lazy_walk/fix/clear, in parallel
   if (ivCount[blockIdx.x] == 0u && (longFlag[blockIdx.x] & kFlagRun) == 0u) return;
 
-  // one lane replays the reference's loop over an LDS copy of each 64-position chunk
-  __shared__ uint32_t chunkL[64];
-  __shared__ uint16_t chunkD[64];
-  __shared__ uint8_t chunkB[68];  // bytes c0 - 1 .. c0 + 63
-  __shared__ int s_stop;
+  // the reference's loop replayed in order, wave-uniform: each 64-position chunk's lengths, distances and
+  // "byte equals its predecessor" bits in registers (one lane per position, read and written with
+  // v_readlane / v_writelane), the current shortcut interval in scalar registers (loaded only when the
+  // walk passes it): no memory access on the per-position chain
   Interval* iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
   const uint32_t niv = ivCount[blockIdx.x];
-  if (lane == 0) s_stop = 0;
   uint64_t skip = 0;
   bool lazyEval = false;
   uint32_t prevL = 0, prevD = 0, k0 = 0;  // previous position's match; first interval not yet passed
+  uint64_t ivLo = niv ? iv[0].lo : ~0ull, ivHi = niv ? iv[0].hi : ~0ull;
   for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
     const uint64_t i = c0 + lane;
     const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
-    chunkL[lane] = i <= lastSearch ? L[i] : 0u;
-    chunkD[lane] = i <= lastSearch ? D[i] : (uint16_t)0;
-    chunkB[lane + 1] = in[B.start + i];
-    if (lane == 0) chunkB[0] = c0 > 0 ? in[B.start + c0 - 1] : 0;
-    __syncthreads();
-    if (lane == 0) {
-      for (uint32_t k = 0; k < cnt; k++) {
-        const uint64_t pos = c0 + k, abs = B.start + pos;
-        while (k0 < niv && iv[k0].hi <= abs) k0++;
-        const bool assumed = k0 < niv && abs >= iv[k0].lo;
-        // self-matching (smallz4.h:631-643): the predecessor's distance-1 match, one shorter
-        const bool sc = pos > 0 && chunkB[k + 1] == chunkB[k] && prevD == 1u && prevL > kSameLetter;
-        if (sc != assumed) {
-          // intervals [0, k0) end before this position and were confirmed; the list is edited in place
+    uint32_t vL = i <= lastSearch ? L[i] : 0u;
+    uint32_t vD = i <= lastSearch ? (uint32_t)D[i] : 0u;
+    const bool eq = i > 0 && i < n && in[B.start + i] == in[B.start + i - 1];
+    const uint64_t eqMask = __ballot(eq);
+    bool stop = false;
+    for (uint32_t k = 0; k < cnt; k++) {
+      const uint64_t pos = c0 + k, abs = B.start + pos;
+      while (k0 < niv && ivHi <= abs) {
+        k0++;
+        ivLo = k0 < niv ? iv[k0].lo : ~0ull;
+        ivHi = k0 < niv ? iv[k0].hi : ~0ull;
+      }
+      const bool assumed = k0 < niv && abs >= ivLo;
+      // self-matching (smallz4.h:631-643): the predecessor's distance-1 match, one shorter
+      const bool sc = pos > 0 && ((eqMask >> k) & 1ull) && prevD == 1u && prevL > kSameLetter;
+      if (sc != assumed) {
+        // intervals [0, k0) end before this position and were confirmed; the list is edited in place
+        if (lane == 0) {
           uint32_t m;
           if (sc) {
             // a shortcut nobody assumed: it runs while the copied length stays above MaxSameLetter;
@@ -4087,46 +4090,44 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, con
           }
           ivCount[blockIdx.x] = m;
           atomicOr(status, 2);
-          s_stop = 1;
-          break;
         }
-        uint32_t curL = 0, curD = 0;
-        if (sc) {
-          curL = prevL - 1;
-          curD = 1;
-          chunkL[k] = curL;
-          chunkD[k] = 1;
-        } else {
-          const uint32_t lk = chunkL[k];
-          // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
-          if (lk >= (uint32_t)kMinMatch) {
-            bool search = true;
-            if (skip > 0) {
-              skip--;
-              search = lazyEval;  // a pending lazy evaluation searches one more position
-              lazyEval = false;
-            }
-            if (search) {
-              lazyEval = (skip == 0);
-              skip = lk;
-              curL = lk;
-              curD = chunkD[k];
-            } else {
-              chunkL[k] = 0;  // never searched by the reference
-            }
+        stop = true;
+        break;
+      }
+      uint32_t curL = 0, curD = 0;
+      if (sc) {
+        curL = prevL - 1;
+        curD = 1;
+        vL = wrlane(vL, curL, k);
+        vD = wrlane(vD, 1u, k);
+      } else {
+        const uint32_t lk = rdlane(vL, k);
+        // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
+        if (lk >= (uint32_t)kMinMatch) {
+          bool search = true;
+          if (skip > 0) {
+            skip--;
+            search = lazyEval;  // a pending lazy evaluation searches one more position
+            lazyEval = false;
+          }
+          if (search) {
+            lazyEval = (skip == 0);
+            skip = lk;
+            curL = lk;
+            curD = rdlane(vD, k);
+          } else {
+            vL = wrlane(vL, 0u, k);  // never searched by the reference
           }
         }
-        prevL = curL;
-        prevD = curD;
       }
+      prevL = curL;
+      prevD = curD;
     }
-    __syncthreads();
-    if (s_stop) return;  // another round recomputes this block
+    if (stop) return;  // another round recomputes this block
     if (i <= lastSearch) {
-      L[i] = chunkL[lane];
-      D[i] = chunkD[lane];
+      L[i] = vL;
+      D[i] = (uint16_t)vD;
     }
-    __syncthreads();
   }
 }
 
