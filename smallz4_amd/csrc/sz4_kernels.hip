@@ -427,6 +427,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 #endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
+#ifndef SZ4_BCAST_SAME
+#define SZ4_BCAST_SAME 1  // 0: the below-chunk broadcast reads and tests every candidate's three words
+#endif
 #ifndef SZ4_RUN_PREFIX
 #define SZ4_RUN_PREFIX 1  // 0: k_find extends candidates inside a same-letter run byte by byte (A/B)
 #endif
@@ -1436,6 +1439,10 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // 2. below the chunk: the group that started before it, one uniform candidate per step
       if (!SZ4_SKIP_BCAST && __ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
+        // a chunk whose 64 targets share their first word (inside one wide key group)
+        const uint32_t me0u = rdlane(me0, 0);
+        // (the LDS-window kernel only: in k_find_sorted_hbm the loop costs the registers of a second workgroup per CU)
+        const bool sameMe0 = SZ4_BCAST_SAME && kLds && __ballot(me0 == me0u) == ~0ull;
         int32_t cBase = (int32_t)first - 1;
         uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? belowPre : 0u;
         while (cBase >= gsB && __ballot(run)) {
@@ -1498,6 +1505,23 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
                 if (__ballot(ya == 0u)) hit(true, (uint32_t)(cBase - k), a0, a1, a2);
                 if (__ballot(yb == 0u)) hit(true, (uint32_t)(cBase - k - 1), b0, b1, b2);
               }
+            }
+#endif
+#if SZ4_BCAST_SAME
+            if (kLds && sameMe0) {
+              // every lane holds the same first word: only the block's candidates with that word can pass,
+              // visited nearest first by bit scan, two readlanes each
+              uint64_t todo = __ballot((int32_t)lane < n && f0 == me0u);
+              while (todo) {
+                const uint32_t kk = (uint32_t)__builtin_ctzll(todo);
+                todo &= todo - 1ull;
+#if SZ4_DIAG == 3
+                dB++;
+#endif
+                const uint32_t k1 = rdlane(f1, kk), k2 = rdlane(f2, kk);
+                if (__ballot((((k1 ^ me1) & m1) | ((k2 ^ me2) & m2)) == 0u)) hit(true, (uint32_t)(cBase - (int32_t)kk), me0u, k1, k2);
+              }
+              k = n;
             }
 #endif
             for (; k < n; k++) {
