@@ -427,6 +427,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 #endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
+#ifndef SZ4_FIX_FORCED
+#define SZ4_FIX_FORCED 1  // 0: k_dp_fix walks a segment of forced same-letter matches chunk by chunk
+#endif
 #ifndef SZ4_BCAST_SAME
 #define SZ4_BCAST_SAME 1  // 0: the below-chunk broadcast reads and tests every candidate's three words
 #endif
@@ -5074,8 +5077,28 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
     RunEnd chain;
     uint32_t closedCost = 0;  // closed-form chunk: cost at its end closedE
     int32_t closedE = 0;
+    bool closedRun = false;   // the closed-form chunk is a same-letter run (not a carried chain)
     int32_t runE = -1;        // the last same-letter run end read, and its exact cost
     uint32_t runC = 0;
+    int32_t forcedE = -1;     // the run end forced_below was asked about, and its answer
+    bool forcedOk = false;
+    // positions [lo, top] all take the distance-1 match of a run ending at E unconditionally: 512 per
+    // step, 8 loads in flight per lane
+    auto forced_below = [&](int32_t top, int32_t E) -> bool {
+      for (int32_t b = top; b >= lo; b -= 512) {
+        bool bad = false;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int32_t i = b - 64 * u - (int32_t)lane;
+          const int32_t ic = i >= lo ? i : lo;  // unconditional (clamped) loads
+          const uint32_t l = L[ic];
+          const uint32_t d = (uint32_t)D[ic];
+          bad |= i >= lo && !(l >= kSameLetter && d == 1u && ic + (int32_t)l == E);
+        }
+        if (__ballot(bad)) return false;
+      }
+      return true;
+    };
     bool done = false;
     int32_t maxReach = hi + 64;  // k_dp_fix<true>: highest position read above the segment
     int32_t lowW = hi;           // k_dp_fix<true>: lowest position written
@@ -5123,6 +5146,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         }
         lowW = cl;
       }
+      closedRun = false;
       if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
         auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
@@ -5166,6 +5190,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                      }
                      closedCost = runC;
                      closedE = E0;
+                     closedRun = true;
                      return true;
                    }
                    if (rmq && chain.valid && chain.margin + 2u >= chain.costE + kMarginBias &&
@@ -5187,7 +5212,19 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         const uint64_t upTo = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
         const int32_t rt = (chg & upTo) ? h - (63 - (int32_t)__builtin_clzll(chg & upTo)) : runTop;
         const int32_t need = (int32_t)cR > ip ? (int32_t)cR : ip;
-        const uint64_t cv = __ballot(lane < cnt && cS != 1u && rt >= need);
+        uint64_t cv = __ballot(lane < cnt && cS != 1u && rt >= need);
+#if SZ4_FIX_FORCED
+        // every position from here down to the segment's bottom takes the same run's match unconditionally
+        // (smallz4.h:409-415: length >= MaxSameLetter, distance 1, the same end): its choice is the stored
+        // one and its cost the stored one plus this chunk's (constant) offset -- converged right here
+        if (cv == 0u && closedRun) {
+          if (forcedE != closedE) {
+            forcedE = closedE;
+            forcedOk = forced_below(h - 64, closedE);
+          }
+          if (forcedOk) cv = 1ull;  // lane 0: position h
+        }
+#endif
         const uint32_t last = cv ? (uint32_t)__builtin_ctzll(cv) : cnt - 1u;  // last position processed
         if (lane <= last) {
           S[ip] = cL;
