@@ -4555,10 +4555,8 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
     // that could reach one continues in the general loop below
     uint32_t tFast = 0;
     if (cnt == 64u) {
-      const uint32_t rowMax = row_max(myL);
-      const uint32_t cmax = max(max(rdlane(rowMax, 0), rdlane(rowMax, 16)), max(rdlane(rowMax, 32), rdlane(rowMax, 48)));
 #if SZ4_DP_VEC
-      if (cmax <= 64u && lits + 4u < litBump) {
+      if (__ballot(myL > 64u) == 0 && lits + 4u < litBump) {  // every length <= 64
         // Row-transposed batches.  The window is held as lane 16q + j = cost[i0 + 4j + 4 - q] << 6, so the
         // next batch's window is one DPP row shift with the four new costs entering lane 0 of their own
         // row.  The four positions' candidate keys (64 lanes each) are folded into one register by two
@@ -4670,6 +4668,8 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
         chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
       }
 #else
+      const uint32_t rowMax = row_max(myL);
+      const uint32_t cmax = max(max(rdlane(rowMax, 0), rdlane(rowMax, 16)), max(rdlane(rowMax, 32), rdlane(rowMax, 48)));
       auto fast = [&](auto smallTag) -> uint32_t {
         constexpr bool kSmall = decltype(smallTag)::value;  // every length <= 16: row 0 holds every candidate
 #pragma unroll
