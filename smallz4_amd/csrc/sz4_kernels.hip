@@ -427,6 +427,9 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
 #endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
+#ifndef SZ4_LEAN_SGPR
+#define SZ4_LEAN_SGPR 80  // k_dp_spec_lean's SGPR budget (80: 8 waves per SIMD, the rest spilled to VGPR lanes)
+#endif
 #ifndef SZ4_FIX_FORCED
 #define SZ4_FIX_FORCED 1  // 0: k_dp_fix walks a segment of forced same-letter matches chunk by chunk
 #endif
@@ -4880,7 +4883,7 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
       uint32_t *__restrict__ costAll, uint32_t *__restrict__ sel, uint32_t *__restrict__ reach,            \
       uint4 *__restrict__ segState, const uint32_t *__restrict__ longFlag, uint32_t *__restrict__ upAll,   \
       uint32_t *__restrict__ downAll
-__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(80))) void k_dp_spec_lean(SZ4_DP_SPEC_ARGS)
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4_LEAN_SGPR))) void k_dp_spec_lean(SZ4_DP_SPEC_ARGS)
 {
   dp_spec_body<false>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
