@@ -2154,6 +2154,22 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
   int32_t* skip = reinterpret_cast<int32_t*>(skipAll + S.elemOff);
   const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
   const uint32_t niv = ivCount[S.block];
+  if (fixMode) {
+    // the repair pass has work only where a piece head's speculative carry differs from its
+    // predecessor's final result (the same test as below): otherwise leave before staging the window
+    bool any = false;
+    if (segLong[blockIdx.x] != 0u) {
+      for (uint64_t q0 = S.s0 + kPiece * (1u + tid); q0 < S.s1; q0 += (uint64_t)kPiece * kFindThreads) {
+        const uint64_t i0 = q0 - matchBase, i1 = q0 - 1 - matchBase;
+        if (!((longBits[i0 >> 5] >> (i0 & 31)) & 1u) || !((longBits[i1 >> 5] >> (i1 & 31)) & 1u)) continue;
+        const uint32_t sd = specDist[q0 - matchBase];
+        if (sd == 0u) continue;
+        if (mlen[q0 - 1 - matchBase] == specLen[q0 - matchBase] && mdist[q0 - 1 - matchBase] == sd) continue;
+        any = true;
+      }
+    }
+    if (__syncthreads_or(any ? 1 : 0) == 0) return;
+  }
 
   // positions not inserted into the chains: shortcut intervals of this block and the previous one
   if (tid == 0) {
