@@ -5904,8 +5904,11 @@ __global__ __launch_bounds__(kAsmThreads) void k_block_bytes(const Block* __rest
   }
 }
 
+#ifndef SZ4_WRITE_WAVES
+#define SZ4_WRITE_WAVES 1  // k_write_seg's minimum waves per SIMD (launch bound): 1 leaves its registers free (77: 6 waves)
+#endif
 // one wavefront per sub-segment writes its tokens (or its raw bytes) into the frame
-__global__ __launch_bounds__(64 * kSegWaves) void k_write_seg(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+__global__ __launch_bounds__(64 * kSegWaves, SZ4_WRITE_WAVES) void k_write_seg(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
                                                              const uint2* __restrict__ walkSegs, uint32_t nwalk,
                                                              const uint4* __restrict__ state, const uint4* __restrict__ info,
                                                              const Token* __restrict__ tokAll, const uint32_t* __restrict__ ntokAll,
