@@ -138,6 +138,10 @@ def parse_args(argv=None):
     ap.add_argument("--stream-reps", type=int, default=10, help="stream leg: 100 MB repetitions (10 = 1 GB)")
     ap.add_argument("--no-dict", action="store_true", help="skip the dictionary-mode leg")
     ap.add_argument("--no-shapes", action="store_true", help="skip the other configs (N=1)")
+    ap.add_argument("--no-levels", action="store_true", help="skip the levels leg (-1, -3, -6, -8 on configs[1])")
+    ap.add_argument("--level-steps", type=int, default=3)
+    ap.add_argument("--level-verify-seconds", type=float, default=6.0)
+    ap.add_argument("--level-cpu-seconds", type=float, default=3.0, help="levels leg: budget of each CPU baseline sample")
     ap.add_argument("--shape-steps", type=int, default=3)
     ap.add_argument("--shape-verify-seconds", type=float, default=8.0)
     ap.add_argument("--dry-run", action="store_true",
@@ -495,6 +499,37 @@ def dictionary_leg(run: Runner, no_verify: bool):
             "path": "sz4_lz4 with a dictionary: the data-parallel dictionary finder (sz4_dict.hip), then the usual parse"}
 
 
+LEVELS = (1, 3, 6, 8)
+
+
+def levels_leg(args, run: Runner, data: bytes, bs: int):
+    """configs[1] at the other chain-depth levels the drop-in keeps (smallz4.cpp:232-238: -1..-8 are
+    maxChainLength 1..8; -1..-3 greedy, -4..-6 lazy, both with the reference's skip bookkeeping,
+    smallz4.h:726-744): GPU MB/s, a sampled byte diff against the reference CLI at that level, and the
+    reference's own rate at that level on the host's cores."""
+    import smallz4_amd
+    torch = run.torch
+    res = {}
+    for lv in LEVELS:
+        chain = smallz4_amd.level_to_chain(lv)
+        elapsed, stages, size, out, t_in = run.compress(data, bs, chain, args.level_steps, 1, "none")
+        part = out[:size].cpu().numpy().tobytes()
+        del out, t_in
+        torch.cuda.empty_cache()
+        rec = {"level": f"-{lv}", "max_chain": chain, "MB/s": round(len(data) * args.level_steps / elapsed / 1e6, 2),
+               "ms_per_step": round(elapsed / args.level_steps * 1e3, 3), "steps": args.level_steps, "warmup": 1,
+               "compression_ratio": round((size + 11) / len(data), 5),
+               "stages_ms": {k: round(v, 3) for k, v in stages.items()}}
+        if not args.no_verify:
+            rec.update(verify_sample(part, data, bs, chain, args.verify_threads, args.level_verify_seconds, every=False))
+        if args.cpu_seconds > 0:
+            rec["cpu_baseline"] = cpu_baseline(data, bs, chain, min(args.cpu_seconds, args.level_cpu_seconds))
+        res[f"-{lv}"] = rec
+        print(json.dumps({"levels": f"-{lv}", **rec}), file=sys.stderr, flush=True)
+        del part
+    return {"config": f"configs[1]'s input: {len(data) / 1e6:g} MB as independent {bs}-byte blocks", "levels": res}
+
+
 def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
     """The other single-GPU-sized configs, each measured, diffed on a bounded sample and round-tripped."""
     torch = run.torch
@@ -607,6 +642,10 @@ def main():
     if world == 1 and not args.no_dict and args.level == 9:
         dict_leg = dictionary_leg(run, args.no_verify)
 
+    levels = None
+    if world == 1 and not args.no_levels and args.level == 9 and args.workload == "enwik8" and not args.mb and nbytes:
+        levels = levels_leg(args, run, data, bs)
+
     shapes = None
     if world == 1 and not args.no_shapes and args.level == 9 and args.workload == "enwik8" and not args.mb:
         shapes = shapes_leg(args, run, chain, data)
@@ -691,6 +730,8 @@ def main():
             rec["stream"] = stream_leg
         if dict_leg is not None:
             rec["dictionary"] = dict_leg
+        if levels is not None:
+            rec["levels"] = levels
         if shapes is not None:
             rec["shapes"] = shapes
         # the reference on this host's cores, rank 0, after the timed region (at every N)

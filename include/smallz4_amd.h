@@ -52,7 +52,8 @@ void sz4_destroy(sz4_ctx* ctx);
 /* Process-wide context pool (thread-safe): sz4_acquire hands out an idle context of `device` (creating
  * one when all are busy), sz4_release returns it.  Concurrent callers get different contexts, so
  * calls through the pool are reentrant -- the reference builds a fresh object per call
- * (smallz4.h:56-64).  Pooled contexts live until the process exits. */
+ * (smallz4.h:56-64).  Pooled contexts live until the process exits; one returned holding more device
+ * memory than sz4_set_pool_cap is trimmed first. */
 int sz4_acquire(sz4_ctx** ctx, int device);
 void sz4_release(sz4_ctx* ctx);
 
@@ -64,7 +65,7 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
  * Any n in bounded memory: the blocks are compressed in pieces of at most
- * sz4_set_batch_chunk bytes (256 MiB by default, ~19 GB of scratch).
+ * sz4_set_batch_chunk bytes (256 MiB by default: about 9-12 GB of scratch).
  *
  *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
  *   block_size    1 .. 4 MiB
@@ -119,7 +120,7 @@ int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_by
 void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
- * device scratch is about 60-75 bytes per piece byte.  0 restores the 256 MiB default. */
+ * device scratch is about 35-50 bytes per piece byte.  0 restores the 256 MiB default. */
 void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured
@@ -171,8 +172,28 @@ typedef void (*sz4_send_out)(const unsigned char* data, unsigned int numBytes, v
 int sz4_unlz4_stream(sz4_ctx* ctx, sz4_get_byte get_byte, sz4_send_out send_bytes, const void* dict, uint64_t dict_len,
                      void* user);
 
-/* Device memory (bytes) the context holds: its grow-only scratch, staging and output buffers. */
+/* Device memory (bytes) the context holds: its scratch, staging and output buffers.  Buffers grow on
+ * demand and are kept for the next call of the same kind. */
 uint64_t sz4_device_bytes(sz4_ctx* ctx);
+
+/* Release every device buffer and pinned host buffer the context holds (after its last call has
+ * finished); the next call allocates again.  The context stays valid. */
+void sz4_trim(sz4_ctx* ctx);
+
+/* Bound the context's device memory to `bytes` (0 = no bound, the default).  A call that would grow
+ * past it first releases the buffers it does not use itself -- those kept from calls of another kind:
+ * the stream path's staging, dictionary tables, the decoder's output image -- and fails with
+ * SZ4_E_NOMEM if that is not enough (the decoder then takes its block-by-block mode, which needs about
+ * half the memory of its split mode, before it gives up).  The same release happens, bound or not, when
+ * the device itself runs out of memory. */
+void sz4_set_device_limit(sz4_ctx* ctx, uint64_t bytes);
+
+/* Buffers the context has released under a device bound or device memory pressure (diagnostics). */
+uint64_t sz4_released_buffers(sz4_ctx* ctx);
+
+/* Pooled contexts (sz4_acquire) that hold more than `bytes` of device memory when they are released
+ * are trimmed (sz4_trim) before they go back to the pool.  0 restores the default, 8 GiB. */
+void sz4_set_pool_cap(uint64_t bytes);
 
 /* Dictionary mode: match-finder rounds the last chunk took (the data-parallel finder assumes the
  * same-letter shortcut intervals and reruns a chunk whose results imply others; 1 = none to correct,

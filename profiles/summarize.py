@@ -34,7 +34,7 @@ def short(name: str) -> str:
 
 
 def pmc(path: str):
-    """kernel -> counter -> (sum, launches)"""
+    """kernel -> counter -> (sum, launches); the pseudo-counter "_ns" sums each dispatch's duration"""
     acc = defaultdict(lambda: defaultdict(lambda: [0.0, set()]))
     if not os.path.exists(path):
         return acc
@@ -46,6 +46,10 @@ def pmc(path: str):
             a = acc[k][row["Counter_Name"]]
             a[0] += float(row["Counter_Value"])
             a[1].add(row["Dispatch_Id"])
+            d = acc[k]["_ns"]
+            if row["Dispatch_Id"] not in d[1] and row.get("End_Timestamp"):
+                d[0] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                d[1].add(row["Dispatch_Id"])
     return acc
 
 
@@ -112,6 +116,13 @@ def main():
         fb = None if fe is None else int(round(fe * 1024 * 2))
         wb = None if wr is None else int(round(wr * 1024))
         cycles = avg_ns * 1e-9 * 2.4e9  # MI355X_MICROARCH.md: 2.4 GHz
+        # the clock the kernel actually ran at, from the SQ pass itself: GRBM_GUI_ACTIVE is summed over the
+        # 8 XCDs (MI355X_MICROARCH.md, DVFS give-back), so cycles per launch = GRBM_GUI_ACTIVE / 8, and the
+        # same pass's dispatch durations give the clock
+        grbm = per_launch(sq, k, "GRBM_GUI_ACTIVE")
+        sq_ns = per_launch(sq, k, "_ns")
+        sq_cycles = None if grbm is None else grbm / 8.0
+        clock = None if sq_cycles is None or not sq_ns else sq_cycles / sq_ns
         out = {"kernel": "k_find_sorted", "tag": a.tag,
                "config": {"workload": a.workload, "bytes_per_gpu": a.bytes_per_gpu, "block_size": a.block_size,
                           "level": 9},
@@ -120,10 +131,14 @@ def main():
                "hbm_bytes_per_launch": None if fb is None or wb is None else fb + wb,
                "valu_per_simd_cycle": None if valu is None else round(valu / (cycles * 1024), 4),
                "salu_per_cu_cycle": None if salu is None else round(salu / (cycles * 256), 4),
+               "clock_ghz_measured": None if clock is None else round(clock, 3),
+               "valu_per_simd_cycle_at_clock": None if valu is None or not sq_cycles else round(valu / (sq_cycles * 1024), 4),
+               "salu_per_cu_cycle_at_clock": None if salu is None or not sq_cycles else round(salu / (sq_cycles * 256), 4),
                "method": "rocprofv3 --pmc FETCH_SIZE, --pmc WRITE_SIZE and an SQ pass, each a separate run "
                          "(profiles/collect.sh); FETCH_SIZE doubled per MI355X_MICROARCH.md; WRITE_SIZE as reported; "
                          "issue rates = SQ_INSTS_VALU / (duration x 2.4 GHz x 1024 SIMDs), "
-                         "SQ_INSTS_SALU / (duration x 2.4 GHz x 256 CUs)"}
+                         "SQ_INSTS_SALU / (duration x 2.4 GHz x 256 CUs); the _at_clock rates use the SQ pass's own cycles, "
+                         "GRBM_GUI_ACTIVE / 8 per launch (clock_ghz_measured = those cycles / that pass's dispatch time)"}
         with open(os.path.join(HERE, f"{a.tag}_pmc.json"), "w") as f:
             json.dump(out, f, indent=1)
             f.write("\n")

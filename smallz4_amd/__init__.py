@@ -250,6 +250,18 @@ class Compressor:
         """Device memory held by this context (scratch, staging, output buffers)."""
         return int(self._lib.sz4_device_bytes(self._h))
 
+    def trim(self):
+        """Release every device and pinned host buffer this context holds (sz4_trim)."""
+        self._lib.sz4_trim(self._h)
+
+    def set_device_limit(self, nbytes: int):
+        """Bound this context's device memory (sz4_set_device_limit; 0 = no bound)."""
+        self._lib.sz4_set_device_limit(self._h, int(nbytes))
+
+    def released_buffers(self) -> int:
+        """Buffers released so far under the device bound or memory pressure (sz4_released_buffers)."""
+        return int(self._lib.sz4_released_buffers(self._h))
+
     def dict_rounds(self) -> int:
         """Dictionary mode: match-finder rounds of the last chunk (sz4_dict_rounds; 0xFFFFFFFF: the
         chunk fell back to the in-order replay)."""

@@ -48,6 +48,10 @@ SIGNATURES = {
     "sz4_unlz4": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64)]),
     "sz4_unlz4_device": (_i32, [_vp, _vp, _u64, _vp, _u64, _vp, _u64, ctypes.POINTER(_u64), _vp]),
     "sz4_device_bytes": (_u64, [_vp]),
+    "sz4_trim": (None, [_vp]),
+    "sz4_set_device_limit": (None, [_vp, _u64]),
+    "sz4_released_buffers": (_u64, [_vp]),
+    "sz4_set_pool_cap": (None, [_u64]),
     "sz4_dict_rounds": (_u32, [_vp]),
     "sz4_last_error": (ctypes.c_char_p, [_vp]),
 }

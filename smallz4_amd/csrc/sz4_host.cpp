@@ -17,6 +17,7 @@
 #include <chrono>
 #include <mutex>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <new>
@@ -36,29 +37,74 @@ constexpr uint32_t kDictMaxRounds = 4 * kMaxIv;  // dictionary rounds before the
 
 uint64_t token_capacity(uint64_t n) { return n / 2 + 4; }
 
+// Device scratch accounting of one context: the bytes it holds, an optional limit, and a call counter.
+// A buffer records the call that last reserved it; buffers of earlier calls (another kind of call: the
+// stream path's staging, dictionary tables, decoder images) are the ones a growing call may release.
+struct DevBuf;
+struct Budget {
+  uint64_t used = 0;   // bytes held by the context's DevBufs
+  uint64_t limit = 0;  // 0: none (sz4_set_device_limit)
+  uint64_t gen = 1;    // the current call
+  std::vector<DevBuf*> bufs;
+  uint64_t shedCount = 0;  // buffers released by shed()
+  void (*onShed)(void*) = nullptr;
+  void* owner = nullptr;
+  uint64_t shed();  // releases every buffer the current call has not reserved; returns the bytes freed
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  Budget* bud = nullptr;
+  uint64_t lastGen = 0;
   hipError_t reserve(size_t bytes)
   {
+    if (bud) lastGen = bud->gen;
     if (bytes <= cap) return hipSuccess;
-    if (p) hipFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = bytes + bytes / 8 + 4096;
+    size_t want = bytes + bytes / 32 + 4096;  // slack: a slightly larger next call does not reallocate
+    if (bud && bud->limit) {
+      if (bud->used - cap + want > bud->limit) want = bytes;
+      if (bud->used - cap + want > bud->limit) bud->shed();
+      if (bud->used - cap + want > bud->limit) return hipErrorOutOfMemory;
+    }
+    release();
     hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) cap = want;
+    if (e == hipErrorOutOfMemory && bud && bud->shed()) {
+      (void)hipGetLastError();
+      e = hipMalloc(&p, want);
+    }
+    if (e == hipSuccess) {
+      cap = want;
+      if (bud) bud->used += want;
+    } else {
+      p = nullptr;
+      (void)hipGetLastError();  // the failure is returned, not left sticky for the next runtime call
+    }
     return e;
   }
   void release()
   {
     if (p) hipFree(p);
+    if (bud) bud->used -= cap;
     p = nullptr;
     cap = 0;
   }
   template <class T>
   T* as() const { return static_cast<T*>(p); }
 };
+
+uint64_t Budget::shed()
+{
+  uint64_t freed = 0;
+  for (DevBuf* b : bufs)
+    if (b->p && b->lastGen != gen) {
+      freed += b->cap;
+      b->release();
+      shedCount++;
+    }
+  if (freed && onShed) onShed(owner);
+  return freed;
+}
 
 // pinned host memory (the stream path's chunk buffers), grow-only
 struct HostBuf {
@@ -128,9 +174,25 @@ struct sz4_ctx {
   uint32_t lastChain = 0;
   bool separateSort = false;  // k_sort runs inside k_find_sorted; SZ4_SEPARATE_SORT=1: its own launch
 
-  DevBuf staged, blocks, segs, iv, ivCount, elemA, elemB, rank, mlen, mdist, cost, tokens, ntok, blockBytes, offsets, status;
-  DevBuf dpSegs, sel, reach, segState, walkSegs, walkSlots, walkState, longFlag, rmqUp, rmqDown, longBits, segLong, segTail;
-  DevBuf dpSide, dpRec;        // the parallel parse-boundary repair: saved speculative values, records
+  DevBuf staged, blocks, segs, iv, ivCount, rank, mlen, mdist, cost, ntok, blockBytes, offsets, status;
+  DevBuf dpSegs, reach, segState, walkSegs, walkState, longFlag, longBits, segLong, segTail;
+  DevBuf dpRec;                // the parallel parse-boundary repair's records
+  // One region for the arrays whose lifetimes do not overlap (reserve_all lays it out):
+  //   match search   sort elements A | B  (dead once the search has finished)
+  //   after it       parse choices (sel) | greedy/lazy replay slots, or the parse's range minima UP | DOWN and
+  //                  k_dp_fix's saved speculative values, or the frame tokens | token-walk slots
+  // sel stays live from k_prep (its tail) through the parse to the token walk; the rest are per stage.
+  DevBuf work;
+  uint64_t offElemB = 0, offRmqUp = 0, offRmqDown = 0, offSide = 0, offLazy = 0, offTok = 0, offWalk = 0;
+  uint2* elemA() const { return work.as<uint2>(); }
+  uint2* elemB() const { return reinterpret_cast<uint2*>(work.as<uint8_t>() + offElemB); }
+  uint32_t* sel() const { return work.as<uint32_t>(); }
+  uint32_t* rmqUp() const { return reinterpret_cast<uint32_t*>(work.as<uint8_t>() + offRmqUp); }
+  uint32_t* rmqDown() const { return reinterpret_cast<uint32_t*>(work.as<uint8_t>() + offRmqDown); }
+  uint2* dpSide() const { return reinterpret_cast<uint2*>(work.as<uint8_t>() + offSide); }
+  uint32_t* lazySlots() const { return reinterpret_cast<uint32_t*>(work.as<uint8_t>() + offLazy); }
+  Token* tokens() const { return reinterpret_cast<Token*>(work.as<uint8_t>() + offTok); }
+  uint32_t* walkSlots() const { return reinterpret_cast<uint32_t*>(work.as<uint8_t>() + offWalk); }
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictRuns, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
   uint32_t dictRounds = 0;  // rounds the last dictionary chunk took (~0u: it fell back to the in-order replay)
@@ -138,7 +200,6 @@ struct sz4_ctx {
   uint64_t dictTempBytes = 0;  // rocPRIM radix sort scratch for dictKeys (queried on first use)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
-  DevBuf lazySlots;            // greedy/lazy levels: searched positions per walk sub-segment
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
   uint64_t batchChunk = 256ull << 20;  // sz4_compress_blocks_device: input bytes per internal pipeline run
@@ -152,6 +213,8 @@ struct sz4_ctx {
   uint32_t dictCont = 0, dictShift = 0, dictLow0 = 0;
   DevBuf unBlk, unMeta, unFlags, unFrame, unDict, unOut, unSeq;  // decoder (sz4_unlz4*)
   DevBuf unSubs, unMasks, unImage;  // decoder split mode: sub-segments, their token-start masks, the u32 image
+  DevBuf unIx;                       // decoder: the parallel frame index's candidates and successors
+  bool unIndexSerial = getenv("SZ4_UNLZ4_INDEX") && atoi(getenv("SZ4_UNLZ4_INDEX")) == 0;  // A/B: the one-lane walk
   std::vector<UnBlock> hUn;
   std::vector<UnSub> hSub;
   bool unSplit = false;  // the last planned frame decodes in split mode
@@ -183,13 +246,21 @@ struct sz4_ctx {
   std::mutex* poolMu = nullptr;
   std::vector<sz4_ctx*>* poolIdle = nullptr;
 
+  Budget budget;
+  // a new call: later reserves record it, and a growing call may release what earlier calls left
+  void begin_call()
+  {
+    err.clear();
+    budget.gen++;
+  }
+
   std::vector<DevBuf*> all_buffers()
   {
-    return {&staged, &blocks, &segs, &iv, &ivCount, &elemA, &elemB, &rank, &mlen, &mdist, &cost, &tokens, &ntok,
-            &blockBytes, &offsets, &status, &dpSegs, &sel, &reach, &segState, &walkSegs, &walkSlots, &walkState,
-            &longFlag, &rmqUp, &rmqDown, &longBits, &segLong, &segTail, &dpSide, &dpRec, &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictRuns, &dictLz,
-            &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &lazySlots, &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
-            &unOut, &unSeq, &unSubs, &unMasks, &unImage};
+    return {&staged, &blocks, &segs, &iv, &ivCount, &rank, &mlen, &mdist, &cost, &ntok, &blockBytes, &offsets, &status,
+            &dpSegs, &reach, &segState, &walkSegs, &walkState, &longFlag, &longBits, &segLong, &segTail, &dpRec, &work,
+            &dictLast, &dictPrevH, &dictPrevX, &dictPH, &dictPE, &dictKeys, &dictTemp, &dictSc, &dictSnap, &dictRuns, &dictLz,
+            &chunkOut[0], &chunkOut[1], &stagedS[0], &stagedS[1], &unBlk, &unMeta, &unFlags, &unFrame, &unDict,
+            &unOut, &unSeq, &unSubs, &unMasks, &unImage, &unIx};
   }
 
   int fail(int code, const char* what, hipError_t e = hipSuccess)
@@ -282,6 +353,27 @@ void finish_plan(sz4_ctx* c)
   }
 }
 
+// the shared region's layout for the current plan (sz4_ctx::work); returns its size in bytes
+uint64_t work_layout(sz4_ctx* c, uint64_t stagedBytes)
+{
+  auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+  const uint64_t nb = c->hBlocks.size();
+  const uint64_t elem = al(c->elemTotal * sizeof(uint2) + 64);
+  c->offElemB = elem;
+  const uint64_t findEnd = 2 * elem;
+  const uint64_t selBytes = al(stagedBytes * 4 + 64), rmq = al((stagedBytes + nb + 8) * 4);
+  c->offRmqUp = selBytes;
+  c->offRmqDown = selBytes + rmq;
+  c->offSide = selBytes + 2 * rmq;
+  const uint64_t parseEnd = c->offSide + al(c->hDp.size() * dp_side_positions() * sizeof(uint2) + 64);
+  c->offLazy = selBytes;
+  const uint64_t lazyEnd = c->offLazy + al(c->hWalk.size() * lazy_slots_per_walk() * 4ull + 64);
+  c->offTok = selBytes;
+  c->offWalk = c->offTok + al(c->tokTotal * sizeof(Token) + 64);
+  const uint64_t emitEnd = c->offWalk + al(c->hWalk.size() * 2 * kWalkCap * 4 + 64);
+  return std::max(std::max(findEnd, parseEnd), std::max(lazyEnd, emitEnd));
+}
+
 int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
 {
   const uint64_t nb = c->hBlocks.size();
@@ -290,32 +382,25 @@ int reserve_all(sz4_ctx* c, uint64_t stagedBytes)
       (e = c->segs.reserve(c->hSegs.size() * sizeof(Segment) + 64)) ||
       (e = c->iv.reserve((nb + 1) * kMaxIv * sizeof(Interval) + 64)) ||
       (e = c->ivCount.reserve((nb + 1) * 4 + 64)) ||
-      (e = c->elemA.reserve(c->elemTotal * sizeof(uint2) + 64)) ||
-      (e = c->elemB.reserve(c->elemTotal * sizeof(uint2) + 64)) ||
       (e = c->rank.reserve(c->rankTotal * 4 + 64)) ||
       (e = c->mlen.reserve(stagedBytes * 4 + 64)) ||
       (e = c->mdist.reserve(stagedBytes * 2 + 64)) ||
       (e = c->cost.reserve((stagedBytes + nb + 8) * 4)) ||
-      (e = c->tokens.reserve(c->tokTotal * sizeof(Token) + 64)) ||
       (e = c->ntok.reserve(nb * 4 + 64)) ||
       (e = c->blockBytes.reserve(nb * 4 + 64)) ||
       (e = c->offsets.reserve((nb + 1) * 8 + 64)) ||
       (e = c->status.reserve(64)) ||
       (e = c->dpSegs.reserve(c->hDp.size() * sizeof(DpSeg) + 64)) ||
-      (e = c->sel.reserve(stagedBytes * 4 + 64)) ||
       (e = c->reach.reserve(stagedBytes * 4 + 64)) ||
       (e = c->segState.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
-      (e = c->dpSide.reserve(c->hDp.size() * dp_side_positions() * sizeof(uint2) + 64)) ||
       (e = c->dpRec.reserve(c->hDp.size() * sizeof(uint4) + 64)) ||
       (e = c->walkSegs.reserve(c->hWalk.size() * sizeof(uint2) + 64)) ||
-      (e = c->walkSlots.reserve(c->hWalk.size() * 2 * kWalkCap * 4 + 64)) ||
       (e = c->walkState.reserve(c->hWalk.size() * sizeof(uint4) + 64)) ||
       (e = c->longFlag.reserve(nb * 4 + 64)) ||
       (e = c->longBits.reserve(stagedBytes / 8 + 64)) ||
       (e = c->segLong.reserve(c->hSegs.size() * 4 + 64)) ||
       (e = c->segTail.reserve(c->hSegs.size() * 8 + 64)) ||
-      (e = c->rmqUp.reserve((stagedBytes + nb + 8) * 4)) ||
-      (e = c->rmqDown.reserve((stagedBytes + nb + 8) * 4)))
+      (e = c->work.reserve(work_layout(c, stagedBytes))))
     return c->fail(SZ4_E_NOMEM, "device allocation", e);
   return SZ4_OK;
 }
@@ -374,7 +459,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
     auto serial = [&]() {
       launch_dict(in, dB, nb, maxChain, (uint32_t)c->dictBack, c->dictLegacy, c->dictLast.as<uint32_t>(),
                   c->dictPrevH.as<uint16_t>(), c->dictPrevX.as<uint16_t>(), c->dictCont, c->dictShift, c->dictLow0,
-                  c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel.as<uint32_t>(), c->longFlag.as<uint32_t>(), s);
+                  c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), c->sel(), c->longFlag.as<uint32_t>(), s);
     };
     if (c->dictSerial) {
       serial();  // A/B and tests: the reference's loop replayed in order by one wavefront
@@ -431,7 +516,7 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       A.tempBytes = c->dictTempBytes;
       A.mlen = c->mlen.as<uint32_t>();
       A.mdist = c->mdist.as<uint16_t>();
-      A.sel = c->sel.as<uint32_t>();
+      A.sel = c->sel();
       A.longFlag = c->longFlag.as<uint32_t>();
       A.walkSegs = c->walkSegs.as<uint2>();
       A.nwalk = (uint32_t)c->hWalk.size();
@@ -478,25 +563,31 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
         return c->fail(SZ4_E_DEVICE, "clear matches", e);
       // k_find_sorted sorts its own segment first unless SZ4_SEPARATE_SORT=1
       if (c->separateSort)
-        launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA.as<uint2>(), c->elemB.as<uint2>(), c->rank.as<uint32_t>(), s);
+        launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA(), c->elemB(), c->rank.as<uint32_t>(), s);
     }
     mark(c, 2, s);
     if (maxChain > 0)
-      launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+      launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB(), c->elemA(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
                   nullptr, nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, !c->separateSort, s);
     mark(c, 3, s);
     if (c->stopAfter == 2) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     if (maxChain > 0)
-      launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB.as<uint2>(), c->elemA.as<uint2>(), c->rank.as<uint32_t>(), maxChain,
+      launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB(), c->elemA(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
                   c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->segTail.as<uint64_t>(),
                   c->ldsWindow, c->hybridLds, false, s);
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
-    launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel.as<uint32_t>(),
+    launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel(),
                 c->longFlag.as<uint32_t>(), c->status.as<int>(), s);
     if (maxChain == 0 || maxChain > (uint32_t)kLazyMax) break;
+    // greedy/lazy: the reference's skip bookkeeping in parallel over the assumed shortcut intervals, which
+    // k_lazy_check / k_lazy_correct then compare with the ones the searches imply (blockBytes is free until
+    // the token walk: it holds each block's first difference)
+    launch_lazy(in, dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), dIv, dIvN, c->longFlag.as<uint32_t>(),
+                c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->lazySlots(), c->walkState.as<uint4>(),
+                c->blockBytes.as<uint32_t>(), c->status.as<int>(), s);
     int st = 0;
     if ((e = hipMemcpyAsync(&st, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
       return c->fail(SZ4_E_DEVICE, "prep", e);
@@ -505,26 +596,18 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
     if ((e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
       return c->fail(SZ4_E_DEVICE, "prep", e);
   }
-  if (maxChain > 0 && maxChain <= (uint32_t)kLazyMax && c->dictBack < 0) {
-    // greedy/lazy: the reference's skip bookkeeping, in parallel for blocks without shortcut intervals
-    // (the others were replayed by k_prep); the token walk's state array is free until k_walk
-    if ((e = c->lazySlots.reserve(c->hWalk.size() * lazy_slots_per_walk() * 4ull + 64)))
-      return c->fail(SZ4_E_NOMEM, "lazy replay slots", e);
-    launch_lazy(dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), dIvN, c->longFlag.as<uint32_t>(),
-                c->mlen.as<uint32_t>(), 0, c->lazySlots.as<uint32_t>(), c->walkState.as<uint4>(), c->status.as<int>(), s);
-  }
   launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
-               c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel.as<uint32_t>(), c->reach.as<uint32_t>(),
-               c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp.as<uint32_t>(), c->rmqDown.as<uint32_t>(),
-               c->dpSide.as<uint2>(), c->dpRec.as<uint4>(),
+               c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel(), c->reach.as<uint32_t>(),
+               c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp(), c->rmqDown(),
+               c->dpSide(), c->dpRec.as<uint4>(),
                c->status.as<int>(), s);
   mark(c, 5, s);
   if (c->stopAfter == 4) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   // optimal levels tokenize the parse's choices, greedy/lazy levels the (skip-filtered) matches
-  const uint32_t* chosen = maxChain > (uint32_t)kGreedyMax ? c->sel.as<uint32_t>() : c->mlen.as<uint32_t>();
+  const uint32_t* chosen = maxChain > (uint32_t)kGreedyMax ? c->sel() : c->mlen.as<uint32_t>();
   // the parse's reach array is free by now: it holds each block's concatenated match positions
   launch_emit(in, dB, nb, c->walkSegs.as<uint2>(), (uint32_t)c->hWalk.size(), maxChain, chosen, c->mdist.as<uint16_t>(), 0,
-              c->walkSlots.as<uint32_t>(), c->walkState.as<uint4>(), c->reach.as<uint32_t>(), c->tokens.as<Token>(),
+              c->walkSlots(), c->walkState.as<uint4>(), c->reach.as<uint32_t>(), c->tokens(),
               c->ntok.as<uint32_t>(), c->blockBytes.as<uint32_t>(), c->offsets.as<uint64_t>(), out, hdrLen,
               c->status.as<int>(), s);
   mark(c, 6, s);
@@ -570,7 +653,11 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   for (;;) {
     if ((e = c->unBlk.reserve(maxBlocks * sizeof(UnBlock) + 64)) || (e = c->unMeta.reserve(64)))
       return c->fail(SZ4_E_NOMEM, "decoder scratch", e);
-    launch_unlz4_index(f, n, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
+    // the parallel index (its scratch is about 3n / 8 bytes); the one-lane walk when that does not fit
+    if (!c->unIndexSerial && c->unIx.reserve(unlz4_ix_scratch_bytes(n)) == hipSuccess)
+      launch_unlz4_index_par(f, n, c->unIx.p, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
+    else
+      launch_unlz4_index(f, n, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
     if ((e = hipMemcpyAsync(meta, c->unMeta.p, sizeof meta, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
       return c->fail(SZ4_E_DEVICE, "frame index", e);
     if (meta[1] != 2) break;
@@ -579,6 +666,16 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   const uint32_t nb = (uint32_t)meta[0];
   c->hUn.resize(nb);
   c->unSplit = false;
+  // split mode needs about twice the per-block decoder's scratch (the u32 image, the sub-segment lists):
+  // when it does not fit, or its 31-bit image cannot address the output, the frame decodes block by block
+  auto blockwise = [&]() {
+    for (DevBuf* b : {&c->unSubs, &c->unMasks, &c->unImage}) b->release();
+    const int mode = c->unSplitMode;
+    c->unSplitMode = 0;
+    const int r = unlz4_plan(c, f, n, total, keep, s);
+    c->unSplitMode = mode;
+    return r;
+  };
   if (nb) {
     if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
         (e = hipStreamSynchronize(s)))
@@ -599,8 +696,10 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
     const uint32_t nsub = (uint32_t)c->hSub.size();
     if ((e = c->unSeq.reserve((uint64_t)nsub * 2 * kUnSubCap * sizeof(uint4) + 64)) ||
         (e = c->unSubs.reserve((uint64_t)nsub * sizeof(UnSub) + 64)) ||
-        (e = c->unMasks.reserve((uint64_t)nsub * (kUnSub / 8) + 64)))
-      return c->fail(SZ4_E_NOMEM, "decoder sequences", e);
+        (e = c->unMasks.reserve((uint64_t)nsub * (kUnSub / 8) + 64))) {
+      c->unSeq.release();
+      return blockwise();
+    }
     if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), nb * sizeof(UnBlock), hipMemcpyHostToDevice, s)) ||
         (e = hipMemcpyAsync(c->unSubs.p, c->hSub.data(), nsub * sizeof(UnSub), hipMemcpyHostToDevice, s)))
       return c->fail(SZ4_E_DEVICE, "decoder plan", e);
@@ -633,11 +732,12 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   if (meta[1] != 0 && !ended) return c->fail(SZ4_E_CORRUPT, "invalid or truncated LZ4 frame");
   // the split image addresses output bytes with 31 bits: a larger output decodes block by block
   if (c->unSplit && w >= (uint64_t)kUnRef) {
-    const int mode = c->unSplitMode;
-    c->unSplitMode = 0;
-    const int r = unlz4_plan(c, f, n, total, keep, s);
-    c->unSplitMode = mode;
-    return r;
+    c->unSeq.release();
+    return blockwise();
+  }
+  if (c->unSplit && ((e = c->unImage.reserve(w * 4 + 64)) || (e = c->unFlags.reserve(64)))) {
+    c->unSeq.release();
+    return blockwise();
   }
   *total = w;
   *keep = k;
@@ -654,8 +754,7 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
     const UnBlock& lastB = c->hUn[keep - 1];
     const uint64_t total = lastB.dst + lastB.size;
     const uint32_t nsub = lastB.subFirst + lastB.subCount;
-    if ((e = c->unImage.reserve(total * 4 + 64)) || (e = c->unFlags.reserve(64)))
-      return c->fail(SZ4_E_NOMEM, "decoder image", e);
+    if (c->unImage.cap < total * 4 + 64 || c->unFlags.cap < 64) return c->fail(SZ4_E_NOMEM, "decoder image");
     uint32_t* flag = c->unFlags.as<uint32_t>();
     if ((e = hipMemcpyAsync(c->unBlk.p, c->hUn.data(), keep * sizeof(UnBlock), hipMemcpyHostToDevice, s)))
       return c->fail(SZ4_E_DEVICE, "decoder plan", e);
@@ -1173,6 +1272,11 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   const char* sep = getenv("SZ4_SEPARATE_SORT");
   c->separateSort = sep && sep[0] == '1';
   for (auto& e : c->ev) hipEventCreate(&e);
+  c->budget.bufs = c->all_buffers();
+  for (DevBuf* b : c->budget.bufs) b->bud = &c->budget;
+  c->budget.owner = c;
+  // a released plan buffer may come back at the same address: upload the plan again
+  c->budget.onShed = [](void* o) { static_cast<sz4_ctx*>(o)->uploadedVersion = ~0ull; };
   if (reserve_bytes && c->staged.reserve(reserve_bytes + kPad) != hipSuccess) {
     sz4_destroy(c);
     return SZ4_E_NOMEM;
@@ -1221,12 +1325,36 @@ int sz4_acquire(sz4_ctx** ctx, int device)
   return r;
 }
 
+// pooled contexts holding more device scratch than this are trimmed when they are returned
+static std::atomic<uint64_t> g_poolCap{8ull << 30};
+
 void sz4_release(sz4_ctx* c)
 {
   if (!c || !c->pooled || !c->poolMu) return;
+  if (c->budget.used > g_poolCap.load()) sz4_trim(c);
   std::lock_guard<std::mutex> lock(*c->poolMu);
   c->poolIdle->push_back(c);
 }
+
+void sz4_set_pool_cap(uint64_t bytes) { g_poolCap.store(bytes ? bytes : (8ull << 30)); }
+
+void sz4_trim(sz4_ctx* c)
+{
+  if (!c) return;
+  DeviceGuard guard(c->device);
+  for (hipStream_t x : {c->stream, c->upStream, c->downStream})
+    if (x) hipStreamSynchronize(x);
+  for (DevBuf* b : c->all_buffers()) b->release();
+  for (HostBuf* b : {&c->hostIn[0], &c->hostIn[1], &c->hostOut[0], &c->hostOut[1]}) b->release();
+  c->uploadedVersion = ~0ull;
+}
+
+void sz4_set_device_limit(sz4_ctx* c, uint64_t bytes)
+{
+  if (c) c->budget.limit = bytes;
+}
+
+uint64_t sz4_released_buffers(sz4_ctx* c) { return c ? c->budget.shedCount : 0; }
 
 uint64_t sz4_bound(uint64_t n, uint32_t block_size)
 {
@@ -1248,7 +1376,7 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   if (!c || !out_size || (!d_in && n) || !d_out || block_size == 0 || block_size > kBlockMax || max_chain > 65535 ||
       header < SZ4_HEADER_SMALLZ4 || header > SZ4_HEADER_NONE)
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   // the kernels write the frame in place: refuse a buffer that could be overrun
   if (out_cap < sz4_bound(n, block_size)) return c->fail(SZ4_E_CAPACITY, "out_cap < sz4_bound(n, block_size)");
   DeviceGuard guard(c->device);
@@ -1360,7 +1488,7 @@ int sz4_lz4_stream(sz4_ctx* c, sz4_get_bytes get_bytes, sz4_send_bytes send_byte
 {
   if (!c || !get_bytes || !send_bytes || max_chain > 65535 || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   DeviceGuard guard(c->device);
   return stream_compress(c, get_bytes, send_bytes, max_chain, (const uint8_t*)dict, dict_len, legacy, user);
 }
@@ -1370,7 +1498,7 @@ int sz4_lz4(sz4_ctx* c, const void* in, uint64_t n, uint32_t max_chain, const vo
 {
   if (!c || !out_size || (!in && n) || !out || max_chain > 65535 || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   DeviceGuard guard(c->device);
   // the stream path over memory: the source hands out 64 KiB pieces, the sink appends
   MemSource src{(const uint8_t*)in, n, 0};
@@ -1415,8 +1543,8 @@ int sz4_debug_matches(sz4_ctx* c, uint32_t* len, uint16_t* dist, uint64_t n)
   if (!c || !len || !dist) return SZ4_E_ARG;
   if (n * 4 > c->mlen.cap || n * 2 > c->mdist.cap) return SZ4_E_ARG;
   // after the parse at optimal levels the lengths are the parse's choices
-  const DevBuf& lens = c->stopAfter == 4 && c->lastChain > (uint32_t)kGreedyMax ? c->sel : c->mlen;
-  if (hipMemcpy(len, lens.p, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+  const uint32_t* lens = c->stopAfter == 4 && c->lastChain > (uint32_t)kGreedyMax ? c->sel() : c->mlen.as<uint32_t>();
+  if (hipMemcpy(len, lens, n * 4, hipMemcpyDeviceToHost) != hipSuccess ||
       hipMemcpy(dist, c->mdist.p, n * 2, hipMemcpyDeviceToHost) != hipSuccess)
     return SZ4_E_DEVICE;
   return SZ4_OK;
@@ -1427,7 +1555,7 @@ int sz4_unlz4_device(sz4_ctx* c, const void* d_frame, uint64_t frame_len, const 
 {
   if (!c || !out_size || (!d_frame && frame_len) || (dict_len && !d_dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   DeviceGuard guard(c->device);
   hipStream_t s = (hipStream_t)stream;
   uint64_t total = 0;
@@ -1446,7 +1574,7 @@ int sz4_unlz4(sz4_ctx* c, const void* frame, uint64_t frame_len, const void* dic
 {
   if (!c || !out_size || (!frame && frame_len) || (dict_len && !dict))
     return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   DeviceGuard guard(c->device);
   hipError_t e;
   const uint64_t dl = std::min<uint64_t>(dict_len, 65536);
@@ -1473,7 +1601,7 @@ int sz4_unlz4_stream(sz4_ctx* c, sz4_get_byte get_byte, sz4_send_out send_bytes,
                      void* user)
 {
   if (!c || !get_byte || !send_bytes || (dict_len && !dict)) return c ? c->fail(SZ4_E_ARG, "bad argument") : SZ4_E_ARG;
-  c->err.clear();
+  c->begin_call();
   DeviceGuard guard(c->device);
   try {
     return stream_decompress(c, get_byte, send_bytes, (const uint8_t*)dict, dict_len, user);
@@ -1485,9 +1613,7 @@ int sz4_unlz4_stream(sz4_ctx* c, sz4_get_byte get_byte, sz4_send_out send_bytes,
 uint64_t sz4_device_bytes(sz4_ctx* c)
 {
   if (!c) return 0;
-  uint64_t t = 0;
-  for (const DevBuf* b : c->all_buffers()) t += b->cap;
-  return t;
+  return c->budget.used;
 }
 
 uint32_t sz4_dict_rounds(sz4_ctx* c) { return c ? c->dictRounds : 0u; }

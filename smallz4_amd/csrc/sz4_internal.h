@@ -25,7 +25,7 @@ constexpr uint32_t kFlagRun = 2;   // a distance-1 match longer than MaxSameLett
 constexpr int kStages = 6;  // runs, sort, find (sorted pass), find (long pass), parse, assemble
 
 // device status word bits (one int per pipeline run)
-constexpr int kStPrepRound = 2;   // k_prep corrected a shortcut interval: run sort/find/prep again
+constexpr int kStPrepRound = 2;   // k_lazy_correct corrected a shortcut interval: run sort/find/walk again
 constexpr int kStInvariant = 4;   // a capacity invariant of the walk/token kernels failed: the frame is invalid
 
 // one LZ4 block (all positions absolute byte offsets in the staged input)
@@ -160,17 +160,18 @@ int launch_dict_parallel(const DictArgs& a, hipStream_t s);
 // greedy/lazy levels: dict_lz_mask_bytes_per_walk() bytes per token-walk sub-segment (lzMasks), one
 // uint4 per sub-segment (lzState)
 uint64_t dict_lz_mask_bytes_per_walk();
-// k_prep: tail clearing, greedy/lazy skip replay and shortcut verification; status bit 2 = intervals
-// corrected, run sort/find/prep again
+// k_prep: the tail positions the reference never searches (lengths 0, literal choices)
 void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* sel, const uint32_t* longFlag, int* status,
                  hipStream_t s);
-// greedy/lazy levels: the parallel replay of the reference's skip bookkeeping for blocks without
-// shortcut intervals (k_lazy_walk / k_lazy_fix / k_lazy_clear); slots: lazy_slots_per_walk() u32 per
-// walk sub-segment, state: one uint4 per walk sub-segment
-void launch_lazy(const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk, const uint32_t* ivCount,
-                 const uint32_t* longFlag, uint32_t* mlen, uint64_t matchBase, uint32_t* slots, uint4* state, int* status,
-                 hipStream_t s);
+// greedy/lazy levels: the parallel replay of the reference's skip bookkeeping (k_lazy_walk / k_lazy_fix /
+// k_lazy_clear) over the assumed same-letter shortcut intervals, then their check (k_lazy_check /
+// k_lazy_correct: status kStPrepRound = an interval list was corrected, run sort/find/walk again);
+// slots: lazy_slots_per_walk() u32 per walk sub-segment, state: one uint4 per walk sub-segment,
+// firstBad: one u32 per block
+void launch_lazy(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
+                 Interval* iv, uint32_t* ivCount, const uint32_t* longFlag, uint32_t* mlen, const uint16_t* mdist,
+                 uint64_t matchBase, uint32_t* slots, uint4* state, uint32_t* firstBad, int* status, hipStream_t s);
 uint32_t lazy_slots_per_walk();
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
                   const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
@@ -214,6 +215,12 @@ struct UnSub {
   uint32_t pad;
 };
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s);
+// the same result from the parallel index (candidate offsets, then one wavefront over their successors;
+// falls back to the serial walk in the same launch when the candidates cannot settle the chain)
+void launch_unlz4_index_par(const uint8_t* f, uint64_t n, void* scratch, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta,
+                            hipStream_t s);
+uint64_t unlz4_ix_scratch_bytes(uint64_t n);
+uint64_t unlz4_ix_cap(uint64_t n);
 // sequence list: unlz4_seq_entries(frame length, blocks) uint4 entries (block bi's at src / 3 + 2 bi)
 uint64_t unlz4_seq_entries(uint64_t frameLen, uint32_t nb);
 void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, uint4* seq, hipStream_t s);

@@ -4045,13 +4045,10 @@ void launch_dict(const uint8_t* in, const Block* blocks, uint32_t nblocks, uint3
                        prevX, cont, shift, low0, mlen, mdist, sel, longFlag);
 }
 
-// Greedy/lazy levels (maxChain <= 6) search only some positions, so where a same-letter shortcut
-// starts depends on the skip state (smallz4.h:631-643, 726-744): the interval k_runs assumed (the
-// run's first position) may start later, or not at all.  k_prep replays the reference's loop in order
-// -- self-match check first, then the skip bookkeeping -- and compares every shortcut position with
-// the assumed intervals.  At the first disagreement it corrects that interval (later positions were
-// searched against the wrong chains) and asks the host for another sort/find/prep round; the checked
-// prefix grows every round.
+// k_prep: the positions the reference never searches -- the last 12 of a block keep length 0, the parse's
+// choices of the last 5 are literals.  (Greedy/lazy levels then replay the reference's skip bookkeeping in
+// parallel: k_lazy_walk / k_lazy_fix / k_lazy_clear, checked against the assumed shortcut intervals by
+// k_lazy_check / k_lazy_correct.)
 __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
                                              Interval* __restrict__ ivAll, uint32_t* __restrict__ ivCount,
                                              uint32_t maxChain, uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
@@ -4074,132 +4071,23 @@ __global__ __launch_bounds__(64) void k_prep(const uint8_t* __restrict__ in, con
     const uint64_t from = n > (uint64_t)kTailNoMatch ? n - kTailLiterals : 0;
     for (uint64_t i = from + lane; i < n; i += 64) S[i] = 0;
   }
-  if (maxChain > (uint32_t)kLazyMax || n < (uint64_t)kTailNoMatch) return;
-  // blocks without shortcut intervals or runs beyond MaxSameLetter: k_lazy_walk/fix/clear, in parallel
-  if (ivCount[blockIdx.x] == 0u && (longFlag[blockIdx.x] & kFlagRun) == 0u) return;
-
-  // the reference's loop replayed in order, wave-uniform: each 64-position chunk's lengths, distances and
-  // "byte equals its predecessor" bits in registers (one lane per position, read and written with
-  // v_readlane / v_writelane), the current shortcut interval in scalar registers (loaded only when the
-  // walk passes it): no memory access on the per-position chain
-  Interval* iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
-  const uint32_t niv = ivCount[blockIdx.x];
-  uint64_t skip = 0;
-  bool lazyEval = false;
-  uint32_t prevL = 0, prevD = 0, k0 = 0;  // previous position's match; first interval not yet passed
-  uint64_t ivLo = niv ? iv[0].lo : ~0ull, ivHi = niv ? iv[0].hi : ~0ull;
-  for (uint64_t c0 = 0; c0 <= lastSearch; c0 += 64) {
-    const uint64_t i = c0 + lane;
-    const uint32_t cnt = (uint32_t)(lastSearch - c0 + 1 < 64 ? lastSearch - c0 + 1 : 64);
-    uint32_t vL = i <= lastSearch ? L[i] : 0u;
-    uint32_t vD = i <= lastSearch ? (uint32_t)D[i] : 0u;
-    const bool eq = i > 0 && i < n && in[B.start + i] == in[B.start + i - 1];
-    const uint64_t eqMask = __ballot(eq);
-    bool stop = false;
-    for (uint32_t k = 0; k < cnt; k++) {
-      const uint64_t pos = c0 + k, abs = B.start + pos;
-      while (k0 < niv && ivHi <= abs) {
-        k0++;
-        ivLo = k0 < niv ? iv[k0].lo : ~0ull;
-        ivHi = k0 < niv ? iv[k0].hi : ~0ull;
-      }
-      const bool assumed = k0 < niv && abs >= ivLo;
-      // self-matching (smallz4.h:631-643): the predecessor's distance-1 match, one shorter
-      const bool sc = pos > 0 && ((eqMask >> k) & 1ull) && prevD == 1u && prevL > kSameLetter;
-      if (sc != assumed) {
-        // intervals [0, k0) end before this position and were confirmed; the list is edited in place
-        if (lane == 0) {
-          uint32_t m;
-          if (sc) {
-            // a shortcut nobody assumed: it runs while the copied length stays above MaxSameLetter;
-            // it replaces the assumed intervals it overlaps
-            Interval x;
-            x.lo = abs;
-            x.hi = abs + (prevL - kSameLetter);
-            x.a = abs - 1;
-            x.La = prevL;
-            uint32_t r = k0;
-            while (r < niv && iv[r].lo < x.hi) r++;
-            if (r == k0) {
-              for (uint32_t j = niv < kMaxIv ? niv : kMaxIv - 1; j > k0; j--) iv[j] = iv[j - 1];
-              m = niv < kMaxIv ? niv + 1 : kMaxIv;
-            } else {
-              for (uint32_t j = 0; j < niv - r; j++) iv[k0 + 1 + j] = iv[r + j];
-              m = k0 + 1 + (niv - r);
-            }
-            iv[k0] = x;
-          } else {
-            // an assumed shortcut that does not happen here: dropped (a later position of the run may
-            // start the real one, found in the next round)
-            for (uint32_t j = k0; j + 1 < niv; j++) iv[j] = iv[j + 1];
-            m = niv - 1;
-          }
-          ivCount[blockIdx.x] = m;
-          atomicOr(status, 2);
-        }
-        stop = true;
-        break;
-      }
-      uint32_t curL = 0, curD = 0;
-      if (sc) {
-        curL = prevL - 1;
-        curD = 1;
-        vL = wrlane(vL, curL, k);
-        vD = wrlane(vD, 1u, k);
-      } else {
-        const uint32_t lk = rdlane(vL, k);
-        // positions without an exact predecessor do no bookkeeping (smallz4.h:659-717)
-        if (lk >= (uint32_t)kMinMatch) {
-          bool search = true;
-          if (skip > 0) {
-            skip--;
-            search = lazyEval;  // a pending lazy evaluation searches one more position
-            lazyEval = false;
-          }
-          if (search) {
-            lazyEval = (skip == 0);
-            skip = lk;
-            curL = lk;
-            curD = rdlane(vD, k);
-          } else {
-            vL = wrlane(vL, 0u, k);  // never searched by the reference
-          }
-        }
-      }
-      prevL = curL;
-      prevD = curD;
-    }
-    if (stop) return;  // another round recomputes this block
-    if (i <= lastSearch) {
-      L[i] = vL;
-      D[i] = (uint16_t)vD;
-    }
-  }
 }
 
 // ================================================================================================
-// Greedy/lazy levels in parallel.  Without shortcut intervals and without distance-1 matches longer
-// than MaxSameLetter in the block (no same-letter shortcut can fire, smallz4.h:631-643), the
-// reference's bookkeeping (smallz4.h:726-744) touches only positions that have an exact predecessor
-// ("linked": a match of >= 4 bytes), and it is a chain of searched positions that alternates:
-//   fresh search at q (skip was 0)  -> the next linked position is searched too (lazy evaluation);
-//   lazy search at q                -> the next L(q) linked positions are skipped, the one after is
-//                                      searched fresh.
-// Linked positions that are not searched keep length 0 (the reference never searched there).
+// Greedy/lazy levels in parallel.  The reference's bookkeeping (smallz4.h:726-744) touches only positions
+// that have an exact predecessor ("linked": a match of >= 4 bytes) and are not same-letter shortcut copies
+// (smallz4.h:631-643: the block's assumed intervals, masked out of the walk), and it is a chain of searched
+// positions that alternates:
 // k_lazy_walk walks this chain per 4096-position sub-segment from an assumed start (the
 // sub-segment's first linked position, fresh); k_lazy_fix walks the sub-segments of a block in order
 // and re-walks from the true entry until it meets the speculative walk at the same position in the
 // same mode (from there both are the same walk); k_lazy_clear zeroes the linked positions no walk
-// searched.  Other blocks keep k_prep's serial replay.
+// searched; k_lazy_check / k_lazy_correct compare the shortcut intervals the walk assumed with the ones its
+// searches imply.
 // ================================================================================================
 constexpr int kWalkWaves = 4;         // sub-segments per k_walk / k_lazy_* workgroup
 constexpr uint32_t kLazyCap = 1400;   // searched positions per sub-segment: <= 2 per 6 linked + 2
 constexpr uint32_t kLazyEnd = 0x7FFFFFFFu;
-
-__device__ __forceinline__ bool lazy_fast_block(const uint32_t* ivCount, const uint32_t* longFlag, uint32_t b)
-{
-  return ivCount[b] == 0u && (longFlag[b] & kFlagRun) == 0u;
-}
 
 // the searched-position chain over a register window of lengths: four 64-position windows in
 // registers, loads three windows ahead (as k_walk); wave-uniform state
@@ -4207,11 +4095,31 @@ struct LazyWalker {
   const uint32_t* L;
   uint32_t lastSearch;  // inclusive
   uint32_t wbase, wL, xL1, xL2, xL3;
+  // the block's assumed same-letter shortcut intervals (absolute positions, ascending): their positions copy
+  // their predecessor's match and do no bookkeeping (smallz4.h:631-643), so the walk does not count them
+  const Interval* iv = nullptr;
+  uint32_t niv = 0, k0 = 0;
+  uint64_t bstart = 0;
+  uint64_t wIv = 0;  // lanes of the current window inside an interval
   __device__ __forceinline__ uint32_t ldw(uint32_t b) const
   {
     // unconditional load (clamped index; masked in next()): see k_walk
     const uint32_t i = b + lane_id();
     return L[i <= lastSearch ? i : lastSearch];
+  }
+  // lanes of the window [base, base + 64) inside an interval (intervals lie >= 65 299 positions apart, so
+  // at most two can touch a window); k0 moves forward with the windows
+  __device__ __forceinline__ uint64_t ivmask(uint32_t base)
+  {
+    while (k0 < niv && iv[k0].hi - bstart <= (uint64_t)base) k0++;
+    uint64_t m = 0;
+    for (uint32_t k = k0; k < niv && k < k0 + 2; k++) {
+      const uint64_t lo = iv[k].lo - bstart, hi = iv[k].hi - bstart;
+      if (lo >= (uint64_t)base + 64) break;
+      const uint32_t a = lo > base ? (uint32_t)(lo - base) : 0u, b = hi < (uint64_t)base + 64 ? (uint32_t)(hi - base) : 64u;
+      if (a < b) m |= (b - a == 64u ? ~0ull : ((1ull << (b - a)) - 1ull)) << a;
+    }
+    return m;
   }
   __device__ __forceinline__ void start(uint32_t pos)
   {
@@ -4220,6 +4128,8 @@ struct LazyWalker {
     xL1 = ldw(wbase + 64);
     xL2 = ldw(wbase + 128);
     xL3 = ldw(wbase + 192);
+    k0 = 0;
+    wIv = niv ? ivmask(wbase) : 0ull;
   }
   // the need-th (0-based) linked position at or after pos, kLazyEnd when there is none
   __device__ __forceinline__ uint32_t next(uint32_t pos, uint32_t need)
@@ -4232,11 +4142,12 @@ struct LazyWalker {
           xL1 = xL2;
           xL2 = xL3;
           xL3 = ldw(wbase + 192);
+          wIv = niv ? ivmask(wbase) : 0ull;
         } else {
           start(pos);
         }
       }
-      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch && wbase + lane_id() <= lastSearch) & (~0ull << (pos - wbase));
+      const uint64_t mask = __ballot(wL >= (uint32_t)kMinMatch && wbase + lane_id() <= lastSearch) & (~0ull << (pos - wbase)) & ~wIv;
       const uint32_t pc = (uint32_t)__popcll(mask);
       if (need < pc) {
         // the set bit with exactly `need` set bits below it: each lane counts its own (mbcnt)
@@ -4255,8 +4166,8 @@ struct LazyWalker {
 
 __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __restrict__ blocks,
                                                                const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                               const Interval* __restrict__ ivAll,
                                                                const uint32_t* __restrict__ ivCount,
-                                                               const uint32_t* __restrict__ longFlag,
                                                                const uint32_t* __restrict__ mlen, uint64_t matchBase,
                                                                uint32_t* __restrict__ slotsAll, uint4* __restrict__ state)
 {
@@ -4265,7 +4176,6 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   if (idx >= nwalk) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint2 ws = walkSegs[idx];
-  if (!lazy_fast_block(ivCount, longFlag, ws.x)) return;
   const Block B = blocks[ws.x];
   const uint32_t n = (uint32_t)(B.end - B.start);
   if (n < (uint32_t)kTailNoMatch) return;
@@ -4275,6 +4185,9 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   LazyWalker w;
   w.L = mlen + (B.start - matchBase);
   w.lastSearch = n - kTailNoMatch;
+  w.iv = ivAll + (uint64_t)ws.x * kMaxIv;
+  w.niv = ivCount[ws.x];
+  w.bstart = B.start;
   w.start(a);
   uint32_t pos = a, need = 0, mode = 0, m = 0, q;  // mode 0: fresh, 1: lazy
   while (true) {
@@ -4293,14 +4206,13 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   if (lane == 0) state[idx] = make_uint4(kLazyCap, kLazyCap + m, q | (mode << 31), 0u);
 }
 
-__global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ ivCount,
-                                                 const uint32_t* __restrict__ longFlag, const uint32_t* __restrict__ mlen,
+__global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
+                                                 const uint32_t* __restrict__ ivCount, const uint32_t* __restrict__ mlen,
                                                  uint64_t matchBase, uint32_t* __restrict__ slotsAll,
                                                  uint4* __restrict__ state, int* __restrict__ status)
 {
   __shared__ uint32_t spec[kLazyCap];  // the sub-segment's speculative searches
   __shared__ uint32_t fix[kLazyCap];   // the repaired ones in front of them
-  if (!lazy_fast_block(ivCount, longFlag, blockIdx.x)) return;
   const Block B = blocks[blockIdx.x];
   const uint32_t lane = threadIdx.x;
   const uint32_t n = (uint32_t)(B.end - B.start);
@@ -4308,6 +4220,9 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
   LazyWalker w;
   w.L = mlen + (B.start - matchBase);
   w.lastSearch = n - kTailNoMatch;
+  w.iv = ivAll + (uint64_t)blockIdx.x * kMaxIv;
+  w.niv = ivCount[blockIdx.x];
+  w.bstart = B.start;
   w.wbase = 0xFFFFFFC0u;  // no window loaded yet
   uint32_t ex = state[B.walkFirst].z;  // exact exit of sub-segment 0 (walked from the block start)
   uint4 st = state[B.walkFirst + 1];
@@ -4379,8 +4294,8 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
 // the linked positions of a sub-segment that no walk searched get length 0
 __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __restrict__ blocks,
                                                                 const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                                const Interval* __restrict__ ivAll,
                                                                 const uint32_t* __restrict__ ivCount,
-                                                                const uint32_t* __restrict__ longFlag,
                                                                 uint32_t* __restrict__ mlen, uint64_t matchBase,
                                                                 const uint32_t* __restrict__ slotsAll,
                                                                 const uint4* __restrict__ state)
@@ -4391,7 +4306,6 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __r
   if (idx >= nwalk) return;
   const uint32_t lane = threadIdx.x & 63;
   const uint2 ws = walkSegs[idx];
-  if (!lazy_fast_block(ivCount, longFlag, ws.x)) return;
   const Block B = blocks[ws.x];
   const uint32_t n = (uint32_t)(B.end - B.start);
   if (n < (uint32_t)kTailNoMatch) return;
@@ -4408,10 +4322,128 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __r
     const uint32_t q = slots[t] - a;
     atomicOr(&bw[q >> 5], 1u << (q & 31));
   }
+  // positions inside a shortcut interval keep their copied match (written by k_find)
+  LazyWalker w;
+  w.iv = ivAll + (uint64_t)ws.x * kMaxIv;
+  w.niv = ivCount[ws.x];
+  w.bstart = B.start;
   for (uint32_t x0 = a; x0 <= hi; x0 += 64) {
     const uint32_t x = x0 + lane;
-    if (x <= hi && L[x] >= (uint32_t)kMinMatch && !((bw[(x - a) >> 5] >> ((x - a) & 31)) & 1u)) L[x] = 0;
+    const uint64_t inIv = w.niv ? w.ivmask(x0) : 0ull;
+    if (x <= hi && L[x] >= (uint32_t)kMinMatch && !((bw[(x - a) >> 5] >> ((x - a) & 31)) & 1u) && !((inIv >> lane) & 1ull))
+      L[x] = 0;
   }
+}
+
+// The same-letter shortcut intervals the walk ASSUMED (k_runs: from each long run's start, as at -9) against
+// the ones the reference's loop would take given the walk's searches (smallz4.h:631-643): a searched position
+// q whose match is (distance 1, length > MaxSameLetter) with data[q + 1] == data[q] starts one at q + 1.
+// Both sets agree up to their first difference, and so does the walk (it only differs after a position the
+// two treat differently), so the first difference of a block is the reference's: k_lazy_correct edits it
+// into the block's list and the host runs the sort/find/walk round again -- each round settles a longer
+// prefix.  firstBad[b] = block-relative position << 1 | (1: an assumed interval
+// that does not start, 0: one that starts unassumed), ~0u when the block agrees.
+__global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_check(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+                                                                const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                                const Interval* __restrict__ ivAll,
+                                                                const uint32_t* __restrict__ ivCount,
+                                                                const uint32_t* __restrict__ longFlag,
+                                                                const uint32_t* __restrict__ mlen, const uint16_t* __restrict__ mdist,
+                                                                uint64_t matchBase, const uint32_t* __restrict__ slotsAll,
+                                                                const uint4* __restrict__ state, uint32_t* __restrict__ firstBad)
+{
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  const uint32_t niv = ivCount[ws.x];
+  if (niv == 0u && (longFlag[ws.x] & kFlagRun) == 0u) return;  // no distance-1 match above MaxSameLetter
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t lastSearch = n - kTailNoMatch;
+  const uint32_t* L = mlen + (B.start - matchBase);
+  const uint16_t* D = mdist + (B.start - matchBase);
+  const uint8_t* data = in + B.start;
+  const Interval* iv = ivAll + (uint64_t)ws.x * kMaxIv;
+  const uint4 st = state[idx];
+  const uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
+  auto shortcut = [&](uint32_t q) {
+    return D[q] == 1u && L[q] > kSameLetter && q + 1 <= lastSearch && data[q + 1] == data[q];
+  };
+  uint32_t bad = ~0u;
+  // searched positions that start a shortcut: each must be an assumed interval's a
+  for (uint32_t t = st.x + lane; t < st.y; t += 64) {
+    const uint32_t q = slots[t];
+    if (!shortcut(q)) continue;
+    bool assumed = false;
+    for (uint32_t j = 0; j < niv && !assumed; j++) assumed = iv[j].lo - B.start == (uint64_t)q + 1;
+    if (!assumed) bad = min(bad, (q + 1) << 1);
+  }
+  // assumed intervals whose a lies in this sub-segment: a must be searched (binary search in the slot list)
+  // and start a shortcut
+  const uint32_t a0 = ws.y * kWalkSeg, a1 = a0 + kWalkSeg;
+  for (uint32_t j = lane; j < niv; j += 64) {
+    const uint32_t lo = (uint32_t)(iv[j].lo - B.start);
+    if (lo == 0 || lo - 1 < a0 || lo - 1 >= a1) continue;
+    const uint32_t q = lo - 1;
+    uint32_t x = st.x, y = st.y;  // the first slot >= q
+    while (x < y) {
+      const uint32_t mid = (x + y) >> 1;
+      if (slots[mid] < q) x = mid + 1;
+      else y = mid;
+    }
+    if (!(x < st.y && slots[x] == q && shortcut(q))) bad = min(bad, (lo << 1) | 1u);
+  }
+  bad = wave_min_u32(bad);
+  if (lane == 0 && bad != ~0u) atomicMin(&firstBad[ws.x], bad);
+}
+
+// one lane per block: the block's first difference edited into its interval list (as k_prep's serial replay
+// did), and the host asked for another round
+__global__ __launch_bounds__(64) void k_lazy_correct(const Block* __restrict__ blocks, Interval* __restrict__ ivAll,
+                                                     uint32_t* __restrict__ ivCount, const uint32_t* __restrict__ mlen,
+                                                     uint64_t matchBase, const uint32_t* __restrict__ firstBad,
+                                                     int* __restrict__ status)
+{
+  const uint32_t b = blockIdx.x;
+  const uint32_t v = firstBad[b];
+  if (v == ~0u || threadIdx.x != 0) return;
+  const Block B = blocks[b];
+  Interval* iv = ivAll + (uint64_t)b * kMaxIv;
+  const uint32_t niv = ivCount[b];
+  const uint64_t lo = B.start + (v >> 1);
+  uint32_t k0 = 0;  // intervals before this position are confirmed
+  while (k0 < niv && iv[k0].lo < lo) k0++;
+  uint32_t m;
+  if (v & 1u) {
+    // an assumed shortcut that does not happen here: dropped (a later position of the run may start the real
+    // one, found in the next round)
+    for (uint32_t j = k0; j + 1 < niv; j++) iv[j] = iv[j + 1];
+    m = niv - 1;
+  } else {
+    // a shortcut nobody assumed: it runs while the copied length stays above MaxSameLetter; it replaces the
+    // assumed intervals it overlaps
+    const uint32_t La = mlen[lo - 1 - matchBase];
+    Interval x;
+    x.lo = lo;
+    x.hi = lo + (La - kSameLetter);
+    x.a = lo - 1;
+    x.La = La;
+    uint32_t r = k0;
+    while (r < niv && iv[r].lo < x.hi) r++;
+    if (r == k0) {
+      for (uint32_t j = niv < kMaxIv ? niv : kMaxIv - 1; j > k0; j--) iv[j] = iv[j - 1];
+      m = niv < kMaxIv ? niv + 1 : kMaxIv;
+    } else {
+      for (uint32_t j = 0; j < niv - r; j++) iv[k0 + 1 + j] = iv[r + j];
+      m = k0 + 1 + (niv - r);
+    }
+    iv[k0] = x;
+  }
+  ivCount[b] = m;
+  atomicOr(status, kStPrepRound);
 }
 
 constexpr int kSpecWaves = 4;  // independent segments per workgroup (workgroup slots, not LDS, bound occupancy)
@@ -6119,17 +6151,21 @@ void launch_prep(const uint8_t* in, const Block* blocks, uint32_t nblocks, Inter
                        longFlag, status);
 }
 
-void launch_lazy(const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk, const uint32_t* ivCount,
-                 const uint32_t* longFlag, uint32_t* mlen, uint64_t matchBase, uint32_t* slots, uint4* state, int* status,
-                 hipStream_t s)
+void launch_lazy(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
+                 Interval* iv, uint32_t* ivCount, const uint32_t* longFlag, uint32_t* mlen, const uint16_t* mdist,
+                 uint64_t matchBase, uint32_t* slots, uint4* state, uint32_t* firstBad, int* status, hipStream_t s)
 {
   if (!nblocks || !nwalk) return;
   const uint32_t grid = (nwalk + kWalkWaves - 1) / kWalkWaves;
-  hipLaunchKernelGGL(k_lazy_walk, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, ivCount, longFlag, mlen,
+  hipLaunchKernelGGL(k_lazy_walk, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, iv, ivCount, mlen,
                      matchBase, slots, state);
-  hipLaunchKernelGGL(k_lazy_fix, dim3(nblocks), dim3(64), 0, s, blocks, ivCount, longFlag, mlen, matchBase, slots, state, status);
-  hipLaunchKernelGGL(k_lazy_clear, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, ivCount, longFlag, mlen,
+  hipLaunchKernelGGL(k_lazy_fix, dim3(nblocks), dim3(64), 0, s, blocks, iv, ivCount, mlen, matchBase, slots, state, status);
+  hipLaunchKernelGGL(k_lazy_clear, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, iv, ivCount, mlen,
                      matchBase, slots, state);
+  hipMemsetAsync(firstBad, 0xFF, (size_t)nblocks * 4, s);
+  hipLaunchKernelGGL(k_lazy_check, dim3(grid), dim3(64 * kWalkWaves), 0, s, in, blocks, walkSegs, nwalk, iv, ivCount, longFlag,
+                     mlen, mdist, matchBase, slots, state, firstBad);
+  hipLaunchKernelGGL(k_lazy_correct, dim3(nblocks), dim3(64), 0, s, blocks, iv, ivCount, mlen, matchBase, firstBad, status);
 }
 
 uint32_t lazy_slots_per_walk() { return 2 * kLazyCap; }

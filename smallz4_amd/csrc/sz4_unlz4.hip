@@ -681,55 +681,67 @@ __device__ uint64_t unlz4_decode_vec(const uint8_t* __restrict__ f, uint64_t n, 
 
 }  // namespace
 
-// one lane walks the size words: meta[0] = blocks found, meta[1] = 0 (frame end reached),
-// 1 (malformed after meta[0] blocks) or 2 (more than maxBlocks), meta[2] = legacy frame
-__global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
-                                                    uint64_t maxBlocks, uint64_t* __restrict__ meta)
+// ---- frame index: the chain of block size words (smallz4cat.c:114-159 header, 189-205 blocks) ------
+// A 4-byte read at any frame offset: two aligned dwords when the frame is 4-byte aligned and they lie
+// inside it, else byte by byte
+__device__ __forceinline__ uint32_t un_rd32(const uint8_t* f, uint64_t n, uint64_t o)
 {
-  if (threadIdx.x != 0) return;
-  // a size word at any offset: two aligned dwords when the frame is 4-byte aligned and they lie inside
-  // it (one load latency per hop of the chain), else byte by byte
-  const bool aligned = (reinterpret_cast<uintptr_t>(f) & 3u) == 0;
-  auto rd32 = [&](uint64_t o) -> uint32_t {
-    const uint64_t a = o & ~3ull;
-    if (aligned && a + 8 <= n) {
-      const uint32_t* w = reinterpret_cast<const uint32_t*>(f + a);
-      return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
-    }
-    return (uint32_t)f[o] | ((uint32_t)f[o + 1] << 8) | ((uint32_t)f[o + 2] << 16) | ((uint32_t)f[o + 3] << 24);
-  };
-  uint64_t nb = 0, st = 0, r = 4;
-  bool legacy = false, blockSum = false;
+  const uint64_t a = o & ~3ull;
+  if ((reinterpret_cast<uintptr_t>(f) & 3u) == 0 && a + 8 <= n) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(f + a);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(o & 3));
+  }
+  return (uint32_t)f[o] | ((uint32_t)f[o + 1] << 8) | ((uint32_t)f[o + 2] << 16) | ((uint32_t)f[o + 3] << 24);
+}
+
+// signature and frame descriptor: the offset of the first size word, or st = 1 (smallz4cat.c:114-159)
+struct UnHeader {
+  uint64_t r0;
+  bool legacy, blockSum;
+  uint32_t st;
+};
+__device__ __forceinline__ UnHeader un_header(const uint8_t* f, uint64_t n)
+{
+  UnHeader h{4, false, false, 0};
   if (n < 4) {
-    st = 1;
-  } else {
-    // signature and frame descriptor (smallz4cat.c:114-159)
-    const uint32_t magic = rd32(0);
-    const bool modern = magic == 0x184D2204u;
-    legacy = magic == 0x184C2102u;
-    if (!modern && !legacy) {
-      st = 1;
-    } else if (modern) {
-      if (r + 1 > n) {
-        st = 1;
-      } else {
-        const uint32_t flg = f[r++];
-        if ((flg >> 6) != 1u) st = 1;
-        blockSum = (flg & 16u) != 0;
-        const uint64_t skip = 1 + ((flg & 8u) ? 8 : 0) + ((flg & 1u) ? 4 : 0) + 1;
-        if (r + skip > n) st = 1;
-        else r += skip;
-      }
+    h.st = 1;
+    return h;
+  }
+  const uint32_t magic = un_rd32(f, n, 0);
+  const bool modern = magic == 0x184D2204u;
+  h.legacy = magic == 0x184C2102u;
+  if (!modern && !h.legacy) {
+    h.st = 1;
+  } else if (modern) {
+    if (h.r0 + 1 > n) {
+      h.st = 1;
+    } else {
+      const uint32_t flg = f[h.r0];
+      if ((flg >> 6) != 1u) h.st = 1;
+      h.blockSum = (flg & 16u) != 0;
+      const uint64_t skip = 1 + ((flg & 8u) ? 8 : 0) + ((flg & 1u) ? 4 : 0) + 1;
+      if (h.r0 + 1 + skip > n) h.st = 1;
+      else h.r0 += 1 + skip;
     }
   }
+  return h;
+}
+
+// the walk in order, one lane: meta[0] = blocks found, meta[1] = 0 (frame end reached), 1 (malformed
+// after meta[0] blocks) or 2 (more than maxBlocks), meta[2] = legacy frame
+__device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk, uint64_t maxBlocks,
+                                   uint64_t* __restrict__ meta)
+{
+  const UnHeader h = un_header(f, n);
+  uint64_t nb = 0, st = h.st, r = h.r0;
   // blocks until the end mark (smallz4cat.c:189-205, 345-349)
   while (st == 0) {
-    if (r == n && legacy) break;
+    if (r == n && h.legacy) break;
     if (r + 4 > n) { st = 1; break; }
-    uint32_t word = rd32(r);
+    uint32_t word = un_rd32(f, n, r);
     r += 4;
-    const bool packed = legacy || (word & 0x80000000u) == 0;
-    if (!legacy) word &= 0x7FFFFFFFu;
+    const bool packed = h.legacy || (word & 0x80000000u) == 0;
+    if (!h.legacy) word &= 0x7FFFFFFFu;
     if (word == 0) break;
     if (r + word > n) { st = 1; break; }
     if (nb == maxBlocks) { st = 2; break; }
@@ -741,14 +753,266 @@ __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ 
     b.stored = packed ? 0u : 1u;
     blk[nb++] = b;
     r += word;
-    if (blockSum) {
+    if (h.blockSum) {
       if (r + 4 > n) { st = 1; break; }
       r += 4;
     }
   }
   meta[0] = nb;
   meta[1] = st;
-  meta[2] = legacy ? 1 : 0;
+  meta[2] = h.legacy ? 1 : 0;
+}
+
+__global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
+                                                    uint64_t maxBlocks, uint64_t* __restrict__ meta)
+{
+  if (threadIdx.x == 0) unlz4_index_serial(f, n, blk, maxBlocks, meta);
+}
+
+// The parallel index.  Every frame offset r >= r0 is classified as if a size word started there:
+//   END    the chain stops cleanly (a zero word; a legacy frame's end, r == n)
+//   BLOCK  a size word whose payload (and block checksum) fits: next(r) = r + 4 + len (+ 4)
+//   BAD    anything else
+// A *candidate* is an offset whose chain stays END/BLOCK for kIxHops hops.  Every size word of a frame
+// the reference reads to its end mark is a candidate, and a random offset almost never is (its "word"
+// must point exactly inside the frame, kIxHops times over), so the true chain is the walk from r0 over
+// the candidates: k_unlz4_ix_cand (a bit per offset, a count per workgroup) -> k_unlz4_ix_scan (workgroup
+// offsets) -> k_unlz4_ix_list (candidates in order, the rank of every bitmap word) -> k_unlz4_ix_walk
+// (each candidate's successor by rank, in parallel; then one wavefront walks the successor array 64
+// entries per register window, v_readlane per hop, and the workgroup writes the blocks).  Whatever the
+// candidates cannot settle -- a bad header, r0 not a candidate, a successor that is not one (a frame
+// that ends malformed), too many candidates -- falls back to the serial walk, so meta is exactly
+// unlz4_index_serial's.
+constexpr uint32_t kIxHops = 3;
+constexpr uint32_t kIxWgWords = 256;  // bitmap words (32 offsets each) per workgroup of k_unlz4_ix_cand
+constexpr uint32_t kIxEnd = 0xFFFFFFFFu, kIxBad = 0xFFFFFFFEu;
+
+__device__ __forceinline__ uint32_t ix_kind(const uint8_t* f, uint64_t n, const UnHeader& h, uint64_t r, uint32_t word,
+                                            uint64_t& next)
+{
+  if (r == n && h.legacy) return kIxEnd;
+  if (r + 4 > n) return kIxBad;
+  if (!h.legacy) word &= 0x7FFFFFFFu;
+  if (word == 0) return kIxEnd;
+  next = r + 4 + word + (h.blockSum ? 4 : 0);
+  return r + 4 + word <= n && next <= n ? 0u : kIxBad;
+}
+
+__device__ __forceinline__ bool ix_candidate(const uint8_t* f, uint64_t n, const UnHeader& h, uint64_t r, uint32_t word)
+{
+  uint64_t next = 0;
+  uint32_t k = ix_kind(f, n, h, r, word, next);
+  for (uint32_t hop = 1; k == 0u && hop < kIxHops; hop++) {
+    r = next;
+    k = ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next);
+  }
+  return k != kIxBad;
+}
+
+// offsets b0 + 32 w + j (j < 32, b0 = r0 rounded down to 4, offsets below r0 left out) of bitmap word w;
+// the span ends at n inclusive (a legacy frame's end)
+__global__ __launch_bounds__(256) void k_unlz4_ix_cand(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
+                                                       uint32_t* __restrict__ bits, uint32_t* __restrict__ wgCount)
+{
+  __shared__ uint32_t s_sum[4];
+  const UnHeader h = un_header(f, n);
+  const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + threadIdx.x;
+  uint32_t m = 0;
+  if (w < nWords && h.st == 0) {
+    const uint64_t p0 = (h.r0 & ~3ull) + 32 * w;
+    const bool fast = (reinterpret_cast<uintptr_t>(f + p0) & 3u) == 0 && p0 + 40 <= n && p0 >= h.r0;
+    if (fast) {
+      // 36 bytes as nine aligned dwords: the 32 words by alignbyte, no further loads for the common BAD
+      const uint32_t* q = reinterpret_cast<const uint32_t*>(f + p0);
+      uint32_t d[9];
+#pragma unroll
+      for (int k = 0; k < 9; k++) d[k] = q[k];
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const uint32_t word = (j & 3) ? __builtin_amdgcn_alignbyte(d[j / 4 + 1], d[j / 4], (uint32_t)(j & 3)) : d[j / 4];
+        if (ix_candidate(f, n, h, p0 + j, word)) m |= 1u << j;
+      }
+    } else {
+      for (int j = 0; j < 32; j++) {
+        const uint64_t r = p0 + j;
+        if (r > n) break;
+        if (r >= h.r0 && ix_candidate(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u)) m |= 1u << j;
+      }
+    }
+    bits[w] = m;
+  }
+  // the workgroup's candidate count
+  uint32_t c = (uint32_t)__popc(m);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
+  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) wgCount[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+}
+
+// exclusive scan of the per-workgroup counts (one workgroup); wgOff[nWg] = the number of candidates
+__global__ __launch_bounds__(1024) void k_unlz4_ix_scan(const uint32_t* __restrict__ wgCount, uint32_t nWg,
+                                                        uint32_t* __restrict__ wgOff)
+{
+  __shared__ uint32_t s_w[16];
+  __shared__ uint32_t s_carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (uint32_t b = 0; b < nWg; b += 1024) {
+    const uint32_t i = b + tid;
+    const uint32_t v = i < nWg ? wgCount[i] : 0u;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    uint32_t before = s_carry;
+    for (uint32_t k = 0; k < wv; k++) before += s_w[k];
+    if (i < nWg) wgOff[i] = before + x - v;
+    __syncthreads();
+    if (tid == 1023) s_carry = before + x;
+    __syncthreads();
+  }
+  if (tid == 0) wgOff[nWg] = s_carry;
+}
+
+// candidates in offset order (list[rank] = offset) and every bitmap word's first rank; nothing is listed
+// beyond `cap` (the walk then falls back)
+__global__ __launch_bounds__(256) void k_unlz4_ix_list(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
+                                                       const uint32_t* __restrict__ bits, const uint32_t* __restrict__ wgOff,
+                                                       uint32_t nWg, uint64_t cap, uint32_t* __restrict__ wordPre,
+                                                       uint64_t* __restrict__ list)
+{
+  __shared__ uint32_t s_w[4];
+  const UnHeader h = un_header(f, n);
+  if (h.st != 0 || (uint64_t)wgOff[nWg] > cap) return;
+  const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + threadIdx.x;
+  const uint32_t m = w < nWords ? bits[w] : 0u;
+  const uint32_t v = (uint32_t)__popc(m), lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) s_w[wv] = x;
+  __syncthreads();
+  uint32_t rank = wgOff[blockIdx.x] + x - v;
+  for (uint32_t k = 0; k < wv; k++) rank += s_w[k];
+  if (w < nWords) wordPre[w] = rank;
+  uint32_t mm = m;
+  while (mm) {
+    const uint32_t j = (uint32_t)__builtin_ctz(mm);
+    mm &= mm - 1u;
+    list[rank++] = (h.r0 & ~3ull) + 32 * w + j;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
+                                                        const uint32_t* __restrict__ bits, const uint32_t* __restrict__ wgOff,
+                                                        uint32_t nWg, uint64_t cap, const uint32_t* __restrict__ wordPre,
+                                                        const uint64_t* __restrict__ list, uint32_t* __restrict__ link,
+                                                        uint32_t* __restrict__ chain, UnBlock* __restrict__ blk,
+                                                        uint64_t maxBlocks, uint64_t* __restrict__ meta)
+{
+  __shared__ uint32_t s_nb, s_st;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const UnHeader h = un_header(f, n);
+  const uint64_t M = wgOff[nWg];
+  // the rank of offset q among the candidates, or kIxBad when q is not one
+  auto rank = [&](uint64_t q) -> uint32_t {
+    if (q < h.r0) return kIxBad;
+    const uint64_t rel = q - (h.r0 & ~3ull), w = rel >> 5;
+    if (w >= nWords) return kIxBad;
+    const uint32_t m = bits[w], b = (uint32_t)(rel & 31);
+    if (!((m >> b) & 1u)) return kIxBad;
+    return wordPre[w] + (uint32_t)__popc(m & ((1u << b) - 1u));
+  };
+  const bool usable = h.st == 0 && M <= cap && M < (uint64_t)kIxBad;
+  // every candidate's successor (kIxEnd: the chain ends there, kIxBad: the next offset is no candidate)
+  if (usable)
+    for (uint64_t i = tid; i < M; i += 1024) {
+      const uint64_t r = list[i];
+      uint64_t next = 0;
+      const uint32_t k = ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next);
+      link[i] = k ? k : rank(next);
+    }
+  __syncthreads();
+  if (tid < 64) {
+    // one wavefront follows the successors from r0: 64 of them per register window, one v_readlane per
+    // hop; the window's successor indices mostly lie in it or the next (prefetched) one
+    uint32_t st = 1, nb = 0;
+    uint32_t i = usable ? rank(h.r0) : kIxBad;
+    i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
+    if (i != kIxBad) {
+      uint64_t base = i & ~63u;
+      uint32_t cur = base + lane < M ? link[base + lane] : kIxBad;
+      uint32_t nxt = base + 64 + lane < M ? link[base + 64 + lane] : kIxBad;
+      uint32_t rec = 0;  // the chain's ranks, 64 per vector store
+      for (;;) {
+        if ((uint64_t)i >= base + 64) {
+          if ((uint64_t)i < base + 128) {
+            base += 64;
+            cur = nxt;
+          } else {
+            base = i & ~63u;
+            cur = base + lane < M ? link[base + lane] : kIxBad;
+          }
+          nxt = base + 64 + lane < M ? link[base + 64 + lane] : kIxBad;
+        }
+        const uint32_t l = un_rdlane(cur, (uint32_t)(i - base));
+        if (l == kIxEnd) {
+          st = 0;
+          break;
+        }
+        if (l == kIxBad) break;  // the serial walk decides
+        if (nb == maxBlocks) {
+          st = 2;
+          break;
+        }
+        rec = un_wrlane(rec, i, nb & 63u);
+        nb++;
+        if ((nb & 63u) == 0) chain[nb - 64 + lane] = rec;
+        i = l;
+      }
+      if (nb & 63u) {
+        const uint32_t b0 = nb & ~63u;
+        if (lane < (nb & 63u)) chain[b0 + lane] = rec;
+      }
+    }
+    if (lane == 0) {
+      s_nb = nb;
+      s_st = st;
+    }
+  }
+  __syncthreads();
+  const uint32_t nb = s_nb, st = s_st;
+  if (st == 1) {
+    if (tid == 0) unlz4_index_serial(f, n, blk, maxBlocks, meta);
+    return;
+  }
+  for (uint32_t k = tid; k < nb; k += 1024) {
+    const uint64_t r = list[chain[k]];
+    uint32_t word = un_rd32(f, n, r);
+    const bool packed = h.legacy || (word & 0x80000000u) == 0;
+    if (!h.legacy) word &= 0x7FFFFFFFu;
+    UnBlock b;
+    b.src = r + 4;
+    b.dst = 0;
+    b.size = 0;
+    b.len = word;
+    b.stored = packed ? 0u : 1u;
+    blk[k] = b;
+  }
+  if (tid == 0) {
+    meta[0] = nb;
+    meta[1] = st;
+    meta[2] = h.legacy ? 1 : 0;
+  }
 }
 
 __global__ __launch_bounds__(64) void k_unlz4_sizes(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
@@ -1043,6 +1307,48 @@ void launch_unlz4_pack(const uint32_t* image, uint64_t total, uint8_t* out, hipS
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s)
 {
   hipLaunchKernelGGL(k_unlz4_index, dim3(1), dim3(64), 0, s, f, n, blk, maxBlocks, meta);
+}
+
+// the parallel index's scratch for a frame of n bytes, carved in this order
+struct IxLayout {
+  uint64_t words, nWg, cap, off[7], total;
+  explicit IxLayout(uint64_t n)
+  {
+    words = n / 32 + 2;  // offsets from r0 rounded down to 4 up to n inclusive
+    nWg = (words + kIxWgWords - 1) / kIxWgWords;
+    cap = unlz4_ix_cap(n);
+    const uint64_t bytes[7] = {4 * words, 4 * words, 4 * (nWg + 1), 4 * (nWg + 1), 8 * cap, 4 * cap, 4 * cap};
+    total = 0;
+    for (int k = 0; k < 7; k++) {
+      off[k] = total;
+      total += (bytes[k] + 255) & ~255ull;
+    }
+  }
+};
+
+uint64_t unlz4_ix_cap(uint64_t n) { return n / 128 + 65536; }
+
+uint64_t unlz4_ix_scratch_bytes(uint64_t n) { return IxLayout(n).total; }
+
+void launch_unlz4_index_par(const uint8_t* f, uint64_t n, void* scratch, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta,
+                            hipStream_t s)
+{
+  const IxLayout L(n);
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  const uint64_t words = L.words, cap = L.cap;
+  const uint32_t nWg = (uint32_t)L.nWg;
+  uint32_t* bits = reinterpret_cast<uint32_t*>(p + L.off[0]);
+  uint32_t* wordPre = reinterpret_cast<uint32_t*>(p + L.off[1]);
+  uint32_t* wgCount = reinterpret_cast<uint32_t*>(p + L.off[2]);
+  uint32_t* wgOff = reinterpret_cast<uint32_t*>(p + L.off[3]);
+  uint64_t* list = reinterpret_cast<uint64_t*>(p + L.off[4]);
+  uint32_t* link = reinterpret_cast<uint32_t*>(p + L.off[5]);
+  uint32_t* chain = reinterpret_cast<uint32_t*>(p + L.off[6]);
+  hipLaunchKernelGGL(k_unlz4_ix_cand, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgCount);
+  hipLaunchKernelGGL(k_unlz4_ix_scan, dim3(1), dim3(1024), 0, s, wgCount, nWg, wgOff);
+  hipLaunchKernelGGL(k_unlz4_ix_list, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list);
+  hipLaunchKernelGGL(k_unlz4_ix_walk, dim3(1), dim3(1024), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list, link,
+                     chain, blk, maxBlocks, meta);
 }
 
 uint64_t unlz4_seq_entries(uint64_t frameLen, uint32_t nb) { return frameLen / 3 + 2ull * nb + 2; }

@@ -89,7 +89,7 @@ CASES = [
     ("dict_zeros_urandom_l9", {"gen": "zeros_urandom_range", "lo": 5 << 20, "n": 6 * M, "seed": 10}, text(65536, 90),
      65535, False),
 ] + [(f"gl_runs_4m_l{_ch}", RUNS_4M, None, _ch, False) for _ch in range(1, 7)] + \
-    [(f"carry_state_l{_ch}", CARRY, None, _ch, False) for _ch in (5, 65535)]
+    [(f"carry_state_l{_ch}", CARRY, None, _ch, False) for _ch in (1, 3, 5, 65535)]
 
 
 def _block_case(args):

@@ -1,6 +1,7 @@
 """Parity of the HIP path (through the C ABI) with the oracle and the reference's golden
 vectors.  Every comparison is byte-for-byte.  Run with -m gpu on an MI355X."""
 import os
+import time
 import subprocess
 
 import numpy as np
@@ -179,9 +180,10 @@ def _matches_fixture(frame, case):
 
 @pytest.mark.parametrize("chain", [1, 2, 3, 4, 5, 6])
 def test_greedy_lazy_long_runs(compressor, chain):
-    """Greedy/lazy levels on same-letter runs > 65299 bytes: k_prep verifies the assumed shortcut
-    intervals and the pipeline reruns until they match the reference's loop (smallz4.h:631-643, 726-744).
-    Against the reference's own frames (tests/golden/streams.json)."""
+    """Greedy/lazy levels on same-letter runs > 65299 bytes: the parallel skip walk runs over the assumed
+    shortcut intervals, k_lazy_check compares them with the ones its searches imply, and the pipeline reruns
+    until they match the reference's loop (smallz4.h:631-643, 726-744).  Against the reference's own frames
+    (tests/golden/streams.json)."""
     for name, data0, bs in ((f"gl_skip_into_run_l{chain}", _skip_into_run(40), 262144),
                             (f"gl_runs_a_l{chain}", synth.enwik8_like(30000, seed=41) + bytes(150000), 262144),
                             (f"gl_runs_b_l{chain}", bytes(70000) + synth.enwik8_like(5000, seed=42) + bytes(90000), 1 << 20)):
@@ -191,6 +193,18 @@ def test_greedy_lazy_long_runs(compressor, chain):
     case, data = _fixture(f"gl_runs_4m_l{chain}")
     assert data == synth.enwik8_like((4 << 20) - 40000, seed=43) + bytes(140000) + synth.enwik8_like(10000, seed=44)
     assert _matches_fixture(compressor.lz4(data, chain), case)
+    if chain in (1, 3, 5):
+        # 21 MB through smallz4::lz4 with zero runs of 120 000 and 90 000 bytes (one across a 4 MiB block
+        # boundary): every block with a run takes the parallel walk and its interval rounds (round 4 replayed
+        # such blocks in one lane: 2.7-2.9 s; the reference on one CPU core: 0.9 s at -1, 2.2 s at -3)
+        case, data = _fixture(f"carry_state_l{chain}")
+        compressor.lz4(data[:1 << 20], chain)
+        t = time.perf_counter()
+        out = compressor.lz4(data, chain)
+        dt = time.perf_counter() - t
+        print(f"carry_state_l{chain}: {len(data) / 1e6:.1f} MB in {dt:.3f} s")
+        assert _matches_fixture(out, case)
+        assert dt < 1.0, dt
 
 
 def test_blocks_long_run_shortcut(compressor):

@@ -103,21 +103,11 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     assert footprint < 24 << 30
 
 
-def test_batch_4gib_one_call_bounded_memory():
+def _batch_4gib(compressor, torch):
     """4 GiB of configs[4]'s shape (zeros/urandom runs, 256 KiB blocks) in ONE sz4_compress_blocks_device
     call: the context's scratch stays under 24 GiB (the call runs 256 MiB pieces), the frame decodes
-    back on the device, every size word walks, and sampled blocks equal the oracle's.  A context of its
-    own: the shared one may hold other tests' stream and dictionary buffers."""
-    import torch
-    import smallz4_amd
-    compressor = smallz4_amd.Compressor(device=0)
-    try:
-        _batch_4gib(compressor, torch)
-    finally:
-        compressor.close()
-
-
-def _batch_4gib(compressor, torch):
+    back on the device, every size word walks, and sampled blocks equal the reference's.  Run by
+    tests/test_memory.py on the shared session context under a 24 GiB device bound."""
     bs = 262144
     lo = 3 << 30
     data = synth.zeros_urandom_range(lo, lo + (4 << 30), seed=10)

@@ -263,3 +263,68 @@ def test_unlz4_split_mode_large_roundtrip(compressor):
     data = synth.silesia_like(24 << 20, seed=74)
     frame = compressor.lz4(data, 65535)
     assert compressor.unlz4(frame) == data
+
+
+def test_unlz4_index_false_candidates(compressor):
+    """The parallel frame index (sz4_unlz4.hip, k_unlz4_ix_*) takes every offset whose size-word chain
+    stays inside the frame for three hops as a candidate.  Stored blocks whose payload is itself an LZ4
+    frame of 1000-byte blocks hold thousands of such chains (and zero words: end marks) next to the true
+    one; the walk from the first size word must step over them.  Modern and legacy outer frames."""
+    text = synth.enwik8_like(400000, seed=74)
+    inner = compressor.compress_blocks(text, 1000, 65535)
+    inner_legacy = compressor.lz4(text, 65535, b"", True)
+    payload = synth.random_bytes(70001, seed=75) + inner + bytes(5) + inner_legacy + inner
+    # (legacy frames at level 1: the reference writes a legacy frame at level 0 with an empty block, see
+    # test_unlz4_golden_streams; its literals still carry the inner frames' size words)
+    for frame in (compressor.compress_blocks(payload, 65536, 0), compressor.compress_blocks(payload, 4099, 0),
+                  compressor.lz4(payload, 1, b"", True), compressor.lz4(payload, 0)):
+        assert check(compressor, frame) == payload
+    # truncated and bit-flipped outer frames: the index decides exactly as the one-lane walk
+    frame = compressor.compress_blocks(payload, 65536, 0)
+    for k in (7, 11, 65540 + 11, len(frame) // 2, len(frame) - 5, len(frame) - 1):
+        check(compressor, frame[:k])
+    for k in (7, 8, 9, 10, 65551):
+        f = bytearray(frame)
+        f[k] ^= 0x40
+        check(compressor, bytes(f))
+
+
+def test_unlz4_index_many_blocks(compressor):
+    """More blocks than the first index attempt takes (65536: the host retries with n / 5 + 2) and more
+    candidates than the parallel index lists (it falls back to the one-lane walk)."""
+    data = synth.enwik8_like(1 << 20, seed=76)
+    frame = compressor.compress_blocks(data, 8, 65535)
+    assert check(compressor, frame) == data
+    frame = compressor.compress_blocks(data, 100, 65535)
+    assert check(compressor, frame) == data
+
+
+def test_unlz4_index_serial_and_parallel_agree(compressor, monkeypatch):
+    """SZ4_UNLZ4_INDEX=0 keeps the one-lane walk (A/B): both index paths give the same output or both
+    reject, on good, truncated and mutated frames."""
+    import smallz4_amd
+    monkeypatch.setenv("SZ4_UNLZ4_INDEX", "0")
+    serial = smallz4_amd.Compressor(device=0)
+    try:
+        rng = np.random.default_rng(77)
+        base = [compressor.compress_blocks(synth.enwik8_like(300000, seed=78), 4096, 65535),
+                compressor.lz4(synth.enwik8_like(300000, seed=79), 9, b"", True)]
+        for i in range(60):
+            f = bytearray(base[i % 2])
+            if i % 3 == 0:
+                f = f[:int(rng.integers(0, len(f)))]
+            else:
+                k = int(rng.integers(4, len(f)))
+                f[k] = int(rng.integers(0, 256))
+            f = bytes(f)
+            try:
+                want = serial.unlz4(f)
+            except NativeError:
+                want = None
+            if want is None:
+                with pytest.raises(NativeError):
+                    compressor.unlz4(f)
+            else:
+                assert compressor.unlz4(f) == want
+    finally:
+        serial.close()
