@@ -436,6 +436,12 @@ constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survive
 #ifndef SZ4_BCAST_SAME
 #define SZ4_BCAST_SAME 1  // 0: the below-chunk broadcast reads and tests every candidate's three words
 #endif
+#ifndef SZ4_BCAST_DPP
+// 1: below-chunk candidates reach the lanes through DPP row_newbcast (16 replicated per register, VGPR-only
+// tests) instead of v_readlane into SGPRs: a VALU instruction with an SGPR operand issues at about 0.63x
+// the rate of one with VGPR operands only (tools/valu_ceiling.hip, profiles/valu_ceiling_r05.json)
+#define SZ4_BCAST_DPP 1
+#endif
 #ifndef SZ4_RUN_PREFIX
 #define SZ4_RUN_PREFIX 1  // 0: k_find extends candidates inside a same-letter run byte by byte (A/B)
 #endif
@@ -846,7 +852,7 @@ __device__ __forceinline__ uint32_t prefix_run(const Src& src, uint64_t p, uint6
 //      lane l holds slot first + l - s, so every lane sees its own candidates in order;
 //   2. candidates below the chunk can only belong to the group that started before it, so they
 //      are the same for all of its lanes: 64 at a time into registers, one v_readlane each.
-// -9 takes the maximum of (prefix << 17 | slot): the reference's nearest-first strict-improvement
+// -9 takes the maximum of (prefix << 17 | position): the reference's nearest-first strict-improvement
 // walk (smallz4.h:190-252) ends on the nearest candidate of maximal prefix, so no order is needed;
 // candidates whose 12 bytes all match are queued per wavefront and extended from the text 64 at a
 // time.  Bounded chains keep the ordered walk (masked "first bestLen+1 bytes" test, strict
@@ -940,7 +946,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   __shared__ uint32_t s_next;
   __shared__ uint32_t s_long;
   __shared__ uint32_t s_tileCnt[kOutTiles];
-  // -9: per wavefront, candidates whose first 12 bytes match (lane << 17 | slot) and the best
+  // -9: per wavefront, candidates whose first 12 bytes match (lane << 17 | position) and the best
   // exact key of each lane among them
   __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
   __shared__ uint32_t s_satBest[kFindThreads / 64][64];
@@ -1148,16 +1154,24 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     if (unlimited) {
       // -9: the reference's nearest-first strict-improvement walk over every candidate ends on
       // the nearest candidate of maximal common prefix, so the result is the maximum of
-      // key = prefix << 17 | slot (slots grow with position inside a group), order-free and
-      // branch-free.  Prefixes are exact up to 12 bytes; candidates reaching 12 are queued and
+      // key = prefix << 17 | position (window-relative), order-free and branch-free.  Prefixes are exact
+      // up to 12 bytes; candidates reaching 12 are queued and
       // extended from the text in batches of 64 (one per lane).
       uint32_t bestKey = SZ4_HIT2 ? 3u << 17 : 0u;  // length 3: no match yet
       uint32_t qn = 0;
       bool walk = false;  // phase 1: this lane still takes candidates inside the chunk
       satBest[lane] = 0;
       const uint32_t cap12 = limit < 12u ? limit : 12u;
+      // keys and queue entries carry the candidate's window-relative POSITION (17 bits): inside one key
+      // group positions ascend with the slots, so the maximum is the same, and no slot array is read to
+      // turn a key into a distance (a global load in the flush would make the compiler wait on the
+      // below-chunk prefetch at every step after it).  Shift-register step sh: the candidate is lane
+      // (lane - sh)'s own position; broadcast candidate k: lane k's fRel
+      auto spos = [&](uint32_t sh) -> uint32_t {
+        return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - sh) & 63u) << 2), (int)myRel);
+      };
       auto flush = [&]() {
-        // lane t extends queue entry base + t: target = lane (e >> 17), candidate slot e & 0x1FFFF
+        // lane t extends queue entry base + t: target = lane (e >> 17), candidate position e & 0x1FFFF
         for (uint32_t base = 0; base < qn; base += 64) {
 #if SZ4_DIAG == 3
         dLi += 1ull << 30;  // flush rounds
@@ -1167,7 +1181,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         const uint32_t tRel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)myRel);
         const uint32_t tLim = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)limit);
         if (base + lane < qn) {
-          const uint64_t tp = S.w0 + tRel, cp = S.w0 + slot_pos(compact, small, cs);
+          const uint64_t tp = S.w0 + tRel, cp = S.w0 + cs;
           uint32_t kk = 12;
           bool open = true;
 #if SZ4_SAT_THRESHOLD
@@ -1277,6 +1291,28 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       auto filt = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
         return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
       };
+      // the hit, from the candidate's words already xor-ed with the lane's own (x0 = 0: same first word)
+      auto hitx = [&](bool mine, uint32_t cs, uint32_t x0, uint32_t x1, uint32_t x2) {
+#if SZ4_DIAG == 3
+        dBi++;  // hit branches (wave-level)
+#endif
+        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
+        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        const uint32_t lcp = min(4u + (z >> 3), cap12);
+        const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
+        bestKey = key > bestKey ? key : bestKey;
+        setMasks();
+        const bool me = mine && (x0 | x1 | x2 | noGrow) == 0u;
+        const uint64_t sat = __ballot(me);
+        if (sat) {
+          const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
+          if (me) satQ[at] = (lane << 17) | cs;
+          qn += (uint32_t)__builtin_popcountll(sat);
+          if (qn >= 64) flush();
+        }
+      };
+      (void)hitx;
       auto hit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
 #if SZ4_DIAG == 3
         dBi++;  // hit branches (wave-level)
@@ -1358,8 +1394,8 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             r2 = shr1(r2);
             const uint32_t yb = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
             if (__ballot(min(ya, yb) == 0u)) {
-              if (__ballot(ya == 0u)) hit(s <= myCnt, slot - s, q0, q1, q2);
-              if (__ballot(yb == 0u)) hit(s + 1u <= myCnt, slot - s - 1u, r0, r1, r2);
+              if (__ballot(ya == 0u)) hit(s <= myCnt, spos(s), q0, q1, q2);
+              if (__ballot(yb == 0u)) hit(s + 1u <= myCnt, spos(s + 1u), r0, r1, r2);
             }
           }
 #endif
@@ -1371,7 +1407,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             r1 = shr1(r1);
             r2 = shr1(r2);
             const uint32_t y = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
-            if (__ballot(y == 0u)) hit(s <= myCnt, slot - s, r0, r1, r2);
+            if (__ballot(y == 0u)) hit(s <= myCnt, spos(s), r0, r1, r2);
           }
         } else {
           for (; s <= trips; s++) {
@@ -1383,7 +1419,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             r2 = shr1(r2);
             const uint32_t dead = s <= myCnt ? 0u : ~0u;
             const uint32_t y = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
-            if (__ballot(y == 0u)) hit(s <= myCnt, slot - s, r0, r1, r2);
+            if (__ballot(y == 0u)) hit(s <= myCnt, spos(s), r0, r1, r2);
           }
         }
 #elif SZ4_SHIFT_UNROLL
@@ -1399,12 +1435,12 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
             r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
             const bool mine = s + u <= myCnt;
-            const uint32_t x = score(mine ? slot - s - u : 0u, mine ? r0 : ~me0, r1, r2);
+            const uint32_t x = score(mine ? spos(s + u) : 0u, mine ? r0 : ~me0, r1, r2);
             xs[u] = mine ? x : 0xFFFFFFFFu;
           }
           if (__ballot(min(xs[0], xs[1]) == 0u) & satOk) {
 #pragma unroll
-            for (uint32_t u = 0; u < 2; u++) enqueue(__ballot(xs[u] == 0u) & satOk, slot - s - u);
+            for (uint32_t u = 0; u < 2; u++) enqueue(__ballot(xs[u] == 0u) & satOk, spos(s + u));
           }
         }
 #endif
@@ -1415,7 +1451,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
           r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
           r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
-          visit(s <= myCnt, slot - s, r0, r1, r2);
+          visit(s <= myCnt, spos(s), r0, r1, r2);
         }
         run = run && (int32_t)gs < (int32_t)first;
       }
@@ -1477,22 +1513,48 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             const uint32_t kc = run ? a : 0u;
             int32_t k = 0;
 #if SZ4_FILTER
+#if SZ4_BCAST_DPP
+            // 16 candidates per register, every row a copy (lane l: candidate q0 + (l & 15)); step K takes
+            // candidate q0 + K to every lane by DPP row_newbcast:K folded into the xor with the lane's word
+            for (int32_t q0 = 0; q0 < n; q0 += 16) {
+              const int src = (int)((uint32_t)(q0 + (int32_t)(lane & 15u)) << 2);
+              const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f0);
+              const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f1);
+              const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f2);
+              const int32_t cnt = n - q0 < 16 ? n - q0 : 16;
+              const uint32_t kcRel = kc > (uint32_t)q0 ? kc - (uint32_t)q0 : 0u;
+#define SZ4_BSTEP_W(K)                                                                                          \
+              if ((K) < cnt) {                                                                                  \
+                const uint32_t x0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g0, 0x150 + (K), 0xF, 0xF, true) ^ me0; \
+                const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g1, 0x150 + (K), 0xF, 0xF, true) ^ me1; \
+                const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g2, 0x150 + (K), 0xF, 0xF, true) ^ me2; \
+                if (__ballot((K) < kcRel && (x0 | (x1 & m1) | (x2 & m2)) == 0u))                                 \
+                  hitx((K) < kcRel, rdlane(fRel, (uint32_t)(q0 + (K))), x0, x1, x2);                                    \
+              }
+              SZ4_BSTEP_W(0) SZ4_BSTEP_W(1) SZ4_BSTEP_W(2) SZ4_BSTEP_W(3) SZ4_BSTEP_W(4) SZ4_BSTEP_W(5)
+              SZ4_BSTEP_W(6) SZ4_BSTEP_W(7) SZ4_BSTEP_W(8) SZ4_BSTEP_W(9) SZ4_BSTEP_W(10) SZ4_BSTEP_W(11)
+              SZ4_BSTEP_W(12) SZ4_BSTEP_W(13) SZ4_BSTEP_W(14) SZ4_BSTEP_W(15)
+#undef SZ4_BSTEP_W
+            }
+            k = n;
+#else
             for (; k < n; k++) {
               const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
-              if (__ballot((uint32_t)k < kc && filt(k0, k1, k2) == 0u)) hit((uint32_t)k < kc, (uint32_t)(cBase - k), k0, k1, k2);
+              if (__ballot((uint32_t)k < kc && filt(k0, k1, k2) == 0u)) hit((uint32_t)k < kc, rdlane(fRel, (uint32_t)k), k0, k1, k2);
             }
 #endif
+#endif
             for (; k + 1 < n; k += 2) {
-              const uint32_t xa = scoreIf((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
-              const uint32_t xb = scoreIf((uint32_t)k + 1u < kc, (uint32_t)(cBase - k - 1), rdlane(f0, k + 1),
+              const uint32_t xa = scoreIf((uint32_t)k < kc, rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              const uint32_t xb = scoreIf((uint32_t)k + 1u < kc, rdlane(fRel, (uint32_t)k + 1u), rdlane(f0, k + 1),
                                           rdlane(f1, k + 1), rdlane(f2, k + 1));
               if (__ballot(min(xa, xb) == 0u) & satOk) {
-                enqueue(__ballot(xa == 0u) & satOk, (uint32_t)(cBase - k));
-                enqueue(__ballot(xb == 0u) & satOk, (uint32_t)(cBase - k - 1));
+                enqueue(__ballot(xa == 0u) & satOk, rdlane(fRel, (uint32_t)k));
+                enqueue(__ballot(xb == 0u) & satOk, rdlane(fRel, (uint32_t)k + 1u));
               }
             }
             if (k < n)
-              visit((uint32_t)k < kc, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              visit((uint32_t)k < kc, rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             if (kc < (uint32_t)n) run = false;
           } else {
             // no window test: every lane may take the candidate (only the group's lanes can match; a
@@ -1508,13 +1570,57 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
               const uint32_t b0 = rdlane(f0, k + 1), b1 = rdlane(f1, k + 1), b2 = rdlane(f2, k + 1);
               const uint32_t ya = filt(a0, a1, a2), yb = filt(b0, b1, b2);
               if (__ballot(min(ya, yb) == 0u)) {
-                if (__ballot(ya == 0u)) hit(true, (uint32_t)(cBase - k), a0, a1, a2);
-                if (__ballot(yb == 0u)) hit(true, (uint32_t)(cBase - k - 1), b0, b1, b2);
+                if (__ballot(ya == 0u)) hit(true, rdlane(fRel, (uint32_t)k), a0, a1, a2);
+                if (__ballot(yb == 0u)) hit(true, rdlane(fRel, (uint32_t)k + 1u), b0, b1, b2);
               }
             }
 #endif
+#if SZ4_BCAST_DPP
+            {
+              // 16 candidates per register, every row a copy (lane l: candidate q0 + (l & 15)); step K takes
+              // candidate q0 + K to every lane by DPP row_newbcast:K folded into the xor with the lane's word.
+              // A chunk whose 64 targets share their first word tests only the candidates with that word
+              // (the others cannot pass): one scalar bit test per candidate, x0 = 0
+              const bool same = SZ4_BCAST_SAME && kLds && sameMe0;
+              const uint64_t todo64 = same ? __ballot((int32_t)lane < n && f0 == me0u) : 0ull;
+              for (int32_t q0 = 0; q0 < n; q0 += 16) {
+                const uint32_t todo = (uint32_t)(todo64 >> q0) & 0xFFFFu;
+                if (same && !todo) continue;
+                const int src = (int)((uint32_t)(q0 + (int32_t)(lane & 15u)) << 2);
+                const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f1);
+                const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f2);
+                const int32_t cnt = n - q0 < 16 ? n - q0 : 16;
+                if (same) {
+#define SZ4_BSTEP_S(K)                                                                                          \
+                  if ((todo >> (K)) & 1u) {                                                                     \
+                    const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g1, 0x150 + (K), 0xF, 0xF, true) ^ me1; \
+                    const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g2, 0x150 + (K), 0xF, 0xF, true) ^ me2; \
+                    if (__ballot(((x1 & m1) | (x2 & m2)) == 0u)) hitx(true, rdlane(fRel, (uint32_t)(q0 + (K))), 0u, x1, x2); \
+                  }
+                  SZ4_BSTEP_S(0) SZ4_BSTEP_S(1) SZ4_BSTEP_S(2) SZ4_BSTEP_S(3) SZ4_BSTEP_S(4) SZ4_BSTEP_S(5)
+                  SZ4_BSTEP_S(6) SZ4_BSTEP_S(7) SZ4_BSTEP_S(8) SZ4_BSTEP_S(9) SZ4_BSTEP_S(10) SZ4_BSTEP_S(11)
+                  SZ4_BSTEP_S(12) SZ4_BSTEP_S(13) SZ4_BSTEP_S(14) SZ4_BSTEP_S(15)
+#undef SZ4_BSTEP_S
+                } else {
+                  const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f0);
+#define SZ4_BSTEP_N(K)                                                                                          \
+                  if ((K) < cnt) {                                                                              \
+                    const uint32_t x0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g0, 0x150 + (K), 0xF, 0xF, true) ^ me0; \
+                    const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g1, 0x150 + (K), 0xF, 0xF, true) ^ me1; \
+                    const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g2, 0x150 + (K), 0xF, 0xF, true) ^ me2; \
+                    if (__ballot((x0 | (x1 & m1) | (x2 & m2)) == 0u)) hitx(true, rdlane(fRel, (uint32_t)(q0 + (K))), x0, x1, x2); \
+                  }
+                  SZ4_BSTEP_N(0) SZ4_BSTEP_N(1) SZ4_BSTEP_N(2) SZ4_BSTEP_N(3) SZ4_BSTEP_N(4) SZ4_BSTEP_N(5)
+                  SZ4_BSTEP_N(6) SZ4_BSTEP_N(7) SZ4_BSTEP_N(8) SZ4_BSTEP_N(9) SZ4_BSTEP_N(10) SZ4_BSTEP_N(11)
+                  SZ4_BSTEP_N(12) SZ4_BSTEP_N(13) SZ4_BSTEP_N(14) SZ4_BSTEP_N(15)
+#undef SZ4_BSTEP_N
+                }
+              }
+              k = n;
+            }
+#endif
 #if SZ4_BCAST_SAME
-            if (kLds && sameMe0) {
+            if (kLds && sameMe0 && k < n) {
               // every lane holds the same first word: only the block's candidates with that word can pass,
               // visited nearest first by bit scan, two readlanes each
               uint64_t todo = __ballot((int32_t)lane < n && f0 == me0u);
@@ -1525,7 +1631,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
                 dB++;
 #endif
                 const uint32_t k1 = rdlane(f1, kk), k2 = rdlane(f2, kk);
-                if (__ballot((((k1 ^ me1) & m1) | ((k2 ^ me2) & m2)) == 0u)) hit(true, (uint32_t)(cBase - (int32_t)kk), me0u, k1, k2);
+                if (__ballot((((k1 ^ me1) & m1) | ((k2 ^ me2) & m2)) == 0u)) hit(true, rdlane(fRel, kk), me0u, k1, k2);
               }
               k = n;
             }
@@ -1535,25 +1641,25 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
               dB++;
 #endif
               const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
-              if (__ballot(filt(k0, k1, k2) == 0u)) hit(true, (uint32_t)(cBase - k), k0, k1, k2);
+              if (__ballot(filt(k0, k1, k2) == 0u)) hit(true, rdlane(fRel, (uint32_t)k), k0, k1, k2);
             }
 #endif
             for (; k + 1 < n; k += 2) {
 #if SZ4_DIAG == 3
               dB += 2;
 #endif
-              const uint32_t xa = score((uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
-              const uint32_t xb = score((uint32_t)(cBase - k - 1), rdlane(f0, k + 1), rdlane(f1, k + 1), rdlane(f2, k + 1));
+              const uint32_t xa = score(rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              const uint32_t xb = score(rdlane(fRel, (uint32_t)k + 1u), rdlane(f0, k + 1), rdlane(f1, k + 1), rdlane(f2, k + 1));
               if (__ballot(min(xa, xb) == 0u) & satOk) {
-                enqueue(__ballot(xa == 0u) & satOk, (uint32_t)(cBase - k));
-                enqueue(__ballot(xb == 0u) & satOk, (uint32_t)(cBase - k - 1));
+                enqueue(__ballot(xa == 0u) & satOk, rdlane(fRel, (uint32_t)k));
+                enqueue(__ballot(xb == 0u) & satOk, rdlane(fRel, (uint32_t)k + 1u));
               }
             }
             for (; k < n; k++) {
 #if SZ4_DIAG == 3
               dB++;
 #endif
-              visit(true, (uint32_t)(cBase - k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
+              visit(true, rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             }
           }
           // settle queued candidates every 256: a lane whose match reached its cap stops there
@@ -1569,7 +1675,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // window test), so it may hold a partial maximum here
       if (bl >= 4u && !big) {
         bestLen = bl;
-        bestDist = (uint32_t)(p - (S.w0 + slot_pos(compact, small, bestKey & 0x1FFFFu)));
+        bestDist = (uint32_t)(p - (S.w0 + (bestKey & 0x1FFFFu)));
         isLong = bl >= limit && limit < room;
       }
     } else {
