@@ -423,7 +423,8 @@ class Runner:
         ok = bool(got == n and torch.equal(dout, t_in))
         del dout, fr
         return ok, {"value": round(n / dt / 1e6, 1), "unit": "MB/s of decoded output (host-timed call: index, sizes "
-                    "and decode launches with their syncs)", "ms": round(dt * 1e3, 3)}
+                    "and decode launches with their syncs)", "ms": round(dt * 1e3, 3),
+                    "split_resolve_passes": self.comp.unlz4_resolve_passes()}
 
 
 def stream_big_leg(data: bytes, reps: int):

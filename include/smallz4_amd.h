@@ -195,10 +195,16 @@ uint64_t sz4_released_buffers(sz4_ctx* ctx);
  * are trimmed (sz4_trim) before they go back to the pool.  0 restores the default, 8 GiB. */
 void sz4_set_pool_cap(uint64_t bytes);
 
-/* Dictionary mode: match-finder rounds the last chunk took (the data-parallel finder assumes the
- * same-letter shortcut intervals and reruns a chunk whose results imply others; 1 = none to correct,
- * 0 = no dictionary chunk yet, UINT32_MAX = the chunk fell back to the in-order replay). */
+/* Dictionary mode: the most match-finder rounds any chunk of the last stream call took (the
+ * data-parallel finder assumes the same-letter shortcut intervals and reruns a chunk whose results imply
+ * others; 1 = none to correct, 0 = no dictionary chunk, UINT32_MAX = a chunk fell back to the in-order
+ * replay: after (largest block / 65 300) + 3 rounds -- one more interval settles per round --, or
+ * SZ4_DICT_MAX_ROUNDS in the environment when the context was created). */
 uint32_t sz4_dict_rounds(sz4_ctx* ctx);
+
+/* Decoder diagnostics: the pointer-jumping passes (k_unlz4_resolve, one host round trip each) the last
+ * decode took in split mode (frames with blocks of >= 256 KiB payload), 0 when it decoded block by block. */
+uint32_t sz4_unlz4_resolve_passes(sz4_ctx* ctx);
 
 /* Last error message of the context ("" if none). */
 const char* sz4_last_error(sz4_ctx* ctx);

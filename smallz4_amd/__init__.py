@@ -267,6 +267,10 @@ class Compressor:
         chunk fell back to the in-order replay)."""
         return int(self._lib.sz4_dict_rounds(self._h))
 
+    def unlz4_resolve_passes(self) -> int:
+        """Pointer-jumping passes of the last split-mode decode (0: decoded block by block)."""
+        return int(self._lib.sz4_unlz4_resolve_passes(self._h))
+
     def set_timing(self, on: bool):
         self._lib.sz4_set_timing(self._h, int(on))
 

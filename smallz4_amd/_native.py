@@ -53,6 +53,7 @@ SIGNATURES = {
     "sz4_released_buffers": (_u64, [_vp]),
     "sz4_set_pool_cap": (None, [_u64]),
     "sz4_dict_rounds": (_u32, [_vp]),
+    "sz4_unlz4_resolve_passes": (_u32, [_vp]),
     "sz4_last_error": (ctypes.c_char_p, [_vp]),
 }
 

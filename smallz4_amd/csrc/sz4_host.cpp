@@ -33,7 +33,11 @@ namespace {
 constexpr uint64_t kPad = 64;                 // bytes of slack after every staged input
 constexpr uint64_t kSegTargets = 65536;       // target positions per segment
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
-constexpr uint32_t kDictMaxRounds = 4 * kMaxIv;  // dictionary rounds before the in-order replay takes the chunk
+// dictionary rounds before the in-order replay takes the chunk: each round settles at least one more
+// shortcut interval of every block, so a chunk needs at most (intervals per block) + 1 rounds, and a block
+// holds at most one interval per MaxSameLetter + 1 bytes; a chunk that needs more than that (ADVICE r04:
+// the old cap was 4 x kMaxIv = 544 rounds) goes to the replay
+uint32_t dict_round_cap(uint64_t maxBlock) { return (uint32_t)(maxBlock / (kSameLetter + 1)) + 3u; }
 
 uint64_t token_capacity(uint64_t n) { return n / 2 + 4; }
 
@@ -195,7 +199,9 @@ struct sz4_ctx {
   uint32_t* walkSlots() const { return reinterpret_cast<uint32_t*>(work.as<uint8_t>() + offWalk); }
   DevBuf dictLast, dictPrevH, dictPrevX;  // dictionary mode: the reference's hash table and both chains
   DevBuf dictPH, dictPE, dictKeys, dictTemp, dictSc, dictSnap, dictRuns, dictLz;  // dictionary mode on the whole GPU (sz4_dict.hip)
-  uint32_t dictRounds = 0;  // rounds the last dictionary chunk took (~0u: it fell back to the in-order replay)
+  uint32_t dictRounds = 0;  // most rounds a dictionary chunk of the last call took (~0u: one fell back to the in-order replay)
+  uint32_t dictMaxRounds = getenv("SZ4_DICT_MAX_ROUNDS") && atoi(getenv("SZ4_DICT_MAX_ROUNDS")) > 0
+                               ? (uint32_t)atoi(getenv("SZ4_DICT_MAX_ROUNDS")) : 0u;  // tests: force the replay (0: dict_round_cap)
   bool dictNoGuess = getenv("SZ4_DICT_NO_GUESS") != nullptr;  // A/B: the first round assumes no shortcut interval
   uint64_t dictTempBytes = 0;  // rocPRIM radix sort scratch for dictKeys (queried on first use)
   DevBuf chunkOut[2];          // stream path: two chunks' blocks (chunk i+1 computes while chunk i downloads)
@@ -218,6 +224,7 @@ struct sz4_ctx {
   std::vector<UnBlock> hUn;
   std::vector<UnSub> hSub;
   bool unSplit = false;  // the last planned frame decodes in split mode
+  uint32_t unResolvePasses = 0;  // pointer-jumping passes the last split-mode decode took
   int unSplitMode = getenv("SZ4_UNLZ4_SPLIT") ? atoi(getenv("SZ4_UNLZ4_SPLIT")) : -1;  // -1 auto, 0 never, 1 always
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
@@ -535,11 +542,11 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
         int st = 0;
         if ((e = hipMemcpyAsync(&st, c->status.p, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
           return c->fail(SZ4_E_DEVICE, "dictionary rounds", e);
-        c->dictRounds = round + 1;
+        if (c->dictRounds != ~0u) c->dictRounds = std::max(c->dictRounds, round + 1);  // sticky over the call's chunks
         if (!(st & (kStPrepRound | kStInvariant))) break;
         if ((e = hipMemsetAsync(c->status.p, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "dictionary rounds", e);
         // every round settles a longer prefix, so this is a safety net, not a path: the in-order replay
-        if ((st & kStInvariant) || round + 1 >= kDictMaxRounds) {
+        if ((st & kStInvariant) || round + 1 >= (c->dictMaxRounds ? c->dictMaxRounds : dict_round_cap(maxBlock))) {
           if ((!c->dictLegacy && (e = tables(false))) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
             return c->fail(SZ4_E_DEVICE, "dictionary tables", e);
           serial();
@@ -553,8 +560,8 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
   }
-  // greedy/lazy levels: k_prep verifies the shortcut intervals k_runs assumed; a corrected block needs
-  // another sort/find/prep round (each round checks a longer prefix of it)
+  // greedy/lazy levels: k_lazy_check verifies the shortcut intervals k_runs assumed; a corrected block
+  // needs another sort/find/walk round (each round checks a longer prefix of it)
   for (uint32_t round = 0; c->dictBack < 0; round++) {
     if (maxChain > 0) {
       // k_find_sorted writes every target (shortcut-interval targets "unresolved", for pass 2); its
@@ -761,7 +768,9 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
     launch_unlz4_split_decode(f, n, c->unBlk.as<UnBlock>(), c->unSubs.as<UnSub>(), nsub, c->unSeq.as<uint4>(),
                               c->unImage.as<uint32_t>(), dict, dl, s);
     // every pass at least halves the longest reference chain (a chain steps to an earlier sub-segment)
+    c->unResolvePasses = 0;
     for (int pass = 0;; pass++) {
+      c->unResolvePasses = (uint32_t)pass + 1;
       uint32_t left = 0;
       if ((e = hipMemsetAsync(flag, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
       launch_unlz4_resolve(c->unImage.as<uint32_t>(), total, flag, s);
@@ -1127,6 +1136,7 @@ int stream_compress_body(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uin
 int stream_compress(sz4_ctx* c, sz4_get_bytes get, sz4_send_bytes send, uint32_t maxChain, const uint8_t* dict,
                     uint64_t dictLen, int legacy, void* user, void* sinkUser = nullptr)
 {
+  c->dictRounds = 0;  // sz4_dict_rounds reports this call's chunks
   try {
     return stream_compress_body(c, get, send, maxChain, dict, dictLen, legacy, user, sinkUser ? sinkUser : user);
   } catch (const std::bad_alloc&) {
@@ -1617,6 +1627,8 @@ uint64_t sz4_device_bytes(sz4_ctx* c)
 }
 
 uint32_t sz4_dict_rounds(sz4_ctx* c) { return c ? c->dictRounds : 0u; }
+
+uint32_t sz4_unlz4_resolve_passes(sz4_ctx* c) { return c && c->unSplit ? c->unResolvePasses : 0u; }
 
 const char* sz4_last_error(sz4_ctx* c) { return c ? c->err.c_str() : "no context"; }
 

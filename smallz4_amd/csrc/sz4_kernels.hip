@@ -7,8 +7,9 @@
 //   k_find_sorted  pass 1, lane = target in sorted order: longest match over its key group
 //                                                                      (smallz4.h:173-255)
 //   k_find_long9 / k_find   pass 2 in text order: long matches, big groups, shortcut intervals
-//   k_prep         never-searched positions; greedy/lazy skip replay and shortcut check
-//                                                                      (smallz4.h:726-744)
+//   k_prep         never-searched tail positions
+//   k_lazy_*       greedy/lazy skip bookkeeping in parallel, shortcut intervals checked
+//                                                                      (smallz4.h:631-643, 726-744)
 //   k_dp_spec / k_dp_fix    backward optimal parse as speculative segments + repair
 //                                                                      (smallz4.h:376-472)
 //   k_walk / k_walk_fix     forward walk of the parse choices          (smallz4.h:259-300)
@@ -81,6 +82,14 @@ __device__ __forceinline__ uint32_t lload4(const uint32_t* w, uint32_t off)
   return __builtin_amdgcn_alignbyte(hi, lo, off & 3);
 }
 
+
+// v_ffbl_b32: index of the lowest set bit, ~0u for 0 (defined, unlike __builtin_ctz)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x)
+{
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 {
@@ -1296,45 +1305,26 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #if SZ4_DIAG == 3
         dBi++;  // hit branches (wave-level)
 #endif
-        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
-        const uint32_t z = min(z1, 32u + min(z2, 32u));
+        // v_ffbl_b32 gives ~0u for 0, so min() takes x2 when x1 is 0 (no compare and select)
+        const uint32_t z = min(ffbl(x1), 32u + min(ffbl(x2), 32u));
         const uint32_t lcp = min(4u + (z >> 3), cap12);
         const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
         bestKey = key > bestKey ? key : bestKey;
         setMasks();
-        const bool me = mine && (x0 | x1 | x2 | noGrow) == 0u;
-        const uint64_t sat = __ballot(me);
+        // queued: 12 bytes equal, and the match may grow past them (the lane's own bit of the ballot, not
+        // the predicate again: one compare instead of a materialised bool compared twice)
+        const uint64_t sat = __ballot(mine && (x0 | x1 | x2 | noGrow) == 0u);
         if (sat) {
           const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
-          if (me) satQ[at] = (lane << 17) | cs;
+          if ((sat >> lane) & 1ull) satQ[at] = (lane << 17) | cs;
           qn += (uint32_t)__builtin_popcountll(sat);
           if (qn >= 64) flush();
         }
       };
-      (void)hitx;
       auto hit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
-#if SZ4_DIAG == 3
-        dBi++;  // hit branches (wave-level)
-#endif
 #if SZ4_HIT2
-        const uint32_t x0 = k0 ^ me0, x1 = k1 ^ me1, x2 = k2 ^ me2;
-        const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
-        const uint32_t z = min(z1, 32u + min(z2, 32u));
-        const uint32_t lcp = min(4u + (z >> 3), cap12);
-        const uint32_t key = (mine && x0 == 0u) ? (lcp << 17) | cs : 0u;
-        bestKey = key > bestKey ? key : bestKey;
-        setMasks();
-        // queued: 12 bytes equal, and the match may grow past them
-        const bool me = mine && (x0 | x1 | x2 | noGrow) == 0u;
-        const uint64_t sat = __ballot(me);
-        if (sat) {
-          const uint32_t at = qn + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(sat >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)sat, 0u));
-          if (me) satQ[at] = (lane << 17) | cs;
-          qn += (uint32_t)__builtin_popcountll(sat);
-          if (qn >= 64) flush();
-        }
+        hitx(mine, cs, k0 ^ me0, k1 ^ me1, k2 ^ me2);
 #else
         const uint32_t x = scoreIf(mine, cs, k0, k1, k2);
         setMasks();
@@ -2195,7 +2185,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict
     const bool rmqLen = lane < cnt && pass1Len == kLongMatch && resLen >= kRmqLen && !(resDist == 1u && resLen >= kSameLetter);
     if (__ballot(rmqLen) && lane == 0) atomicOr(&longFlag[S.block], kFlagRmq);
     // a distance-1 match beyond MaxSameLetter: the next position may take the same-letter shortcut
-    // (smallz4.h:631-643), so the greedy/lazy replay of this block stays in k_prep
+    // (smallz4.h:631-643): at greedy/lazy levels k_lazy_check compares the block's searches with its intervals
     const bool runLen = lane < cnt && pass1Len == kLongMatch && resDist == 1u && resLen > kSameLetter;
     if (__ballot(runLen) && lane == 0) atomicOr(&longFlag[S.block], kFlagRun);
   }
@@ -3489,6 +3479,19 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         r1a = ga + s_cls[e0 + 1];
       }
       uint32_t bestKey = 0;
+#if SZ4_BCAST_DPP
+      // candidates arrive in no particular order (class by class), so the filter lets through those that
+      // reach the current best length (ties are decided by position in the key), all 12 bytes once the
+      // best has 12 or the cap
+      uint32_t m1 = 0, m2 = 0;
+      auto setMasksBig = [&]() {
+        const uint32_t len = bestKey >> 17;
+        const uint32_t bits = len >= cap12 ? 64u : len > 4u ? 8u * (len - 4u) : 0u;
+        const uint64_t mk = bits >= 64u ? ~0ull : (1ull << bits) - 1ull;
+        m1 = (uint32_t)mk;
+        m2 = (uint32_t)(mk >> 32);
+      };
+#endif
       for (int part = 0; part < 2; part++) {
         const uint32_t lo = part == 0 ? r0a : r1a, hi = part == 0 ? r0b : r1b;
         for (uint32_t base = lo; base < hi; base += 64) {
@@ -3498,6 +3501,54 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           const uint64_t cp = S.w0 + (ci < hi ? cr : 0u);
           const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
           const uint32_t n = hi - base < 64u ? hi - base : 64u;
+#if SZ4_BCAST_DPP
+          // 16 candidates per register, every row a copy; step K takes candidate q0 + K to every lane by DPP
+          // row_newbcast:K (VGPR operands only), the exact prefix only when the filter lets it through
+          for (uint32_t q0 = 0; q0 < n; q0 += 16) {
+            const int sl = (int)((q0 + (lane & 15u)) << 2);
+            const uint32_t gce = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)ce);
+            const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)f0);
+            const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)f1);
+            const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)f2);
+            const uint32_t cnt = n - q0 < 16u ? n - q0 : 16u;
+            setMasksBig();
+#define SZ4_BIGSTEP(K)                                                                                          \
+            if ((K) < cnt) {                                                                                    \
+              const uint32_t ej = (uint32_t)__builtin_amdgcn_mov_dpp((int)gce, 0x150 + (K), 0xF, 0xF, true);    \
+              const uint32_t x0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g0, 0x150 + (K), 0xF, 0xF, true) ^ me0; \
+              const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g1, 0x150 + (K), 0xF, 0xF, true) ^ me1; \
+              const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g2, 0x150 + (K), 0xF, 0xF, true) ^ me2; \
+              const uint32_t c = ej & 0x1FFFFu;                                                                 \
+              const bool ok = act && c < pRel && c >= lbRel && (ej >> 17) != exCls;                             \
+              if (__ballot(ok && (x0 | (x1 & m1) | (x2 & m2)) == 0u)) {                                         \
+                const uint32_t z = min(ffbl(x1), 32u + min(ffbl(x2), 32u));                                     \
+                uint32_t lcp = min(4u + (z >> 3), cap12);                                                       \
+                if (ok && x0 == 0u && lcp == 12u && limit > 12u) {                                              \
+                  const uint64_t cc = S.w0 + c;                                                                 \
+                  const uint32_t bl = bestKey >> 17;                                                            \
+                  bool open = !(bl > 12u && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));                     \
+                  while (open && lcp < limit) {                                                                 \
+                    const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);                                    \
+                    if (x) {                                                                                    \
+                      lcp += (uint32_t)__builtin_ctz(x) >> 3;                                                   \
+                      open = false;                                                                             \
+                    } else {                                                                                    \
+                      lcp += 4;                                                                                 \
+                    }                                                                                           \
+                  }                                                                                             \
+                  if (lcp > limit) lcp = limit;                                                                 \
+                }                                                                                               \
+                const uint32_t key = ok && x0 == 0u ? (lcp << 17) | c : 0u;                                     \
+                bestKey = key > bestKey ? key : bestKey;                                                        \
+                setMasksBig();                                                                                  \
+              }                                                                                                 \
+            }
+            SZ4_BIGSTEP(0) SZ4_BIGSTEP(1) SZ4_BIGSTEP(2) SZ4_BIGSTEP(3) SZ4_BIGSTEP(4) SZ4_BIGSTEP(5)
+            SZ4_BIGSTEP(6) SZ4_BIGSTEP(7) SZ4_BIGSTEP(8) SZ4_BIGSTEP(9) SZ4_BIGSTEP(10) SZ4_BIGSTEP(11)
+            SZ4_BIGSTEP(12) SZ4_BIGSTEP(13) SZ4_BIGSTEP(14) SZ4_BIGSTEP(15)
+#undef SZ4_BIGSTEP
+          }
+#else
           for (uint32_t j = 0; j < n; j++) {
             const uint32_t ej = rdlane(ce, j), k0 = rdlane(f0, j), k1 = rdlane(f1, j), k2 = rdlane(f2, j);
             const uint32_t c = ej & 0x1FFFFu;
@@ -3526,6 +3577,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             const uint32_t key = ok ? (lcp << 17) | c : 0u;
             bestKey = key > bestKey ? key : bestKey;
           }
+#endif
         }
       }
       if (act) {
@@ -3671,8 +3723,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
 
 // ================================================================================================
 // The parse, after the matches are known.
-//   k_prep    one wavefront per block: clears the positions the reference never searched and, at
-//             greedy/lazy levels, replays the reference's skip scan (smallz4.h:726-744);
+//   k_prep    one wavefront per block: clears the positions the reference never searched (the
+//             greedy/lazy skip bookkeeping runs before it in k_lazy_*, smallz4.h:726-744);
 //   k_dp_spec one wavefront per DpSeg: the backward optimal parse (estimateCosts,
 //             smallz4.h:376-472) of B.dpSize positions.  The top segment of a block starts from the
 //             block end exactly; every other segment starts from a guessed boundary (costs 0 above

@@ -777,14 +777,14 @@ __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ 
 // the reference reads to its end mark is a candidate, and a random offset almost never is (its "word"
 // must point exactly inside the frame, kIxHops times over), so the true chain is the walk from r0 over
 // the candidates: k_unlz4_ix_cand (a bit per offset, a count per workgroup) -> k_unlz4_ix_scan (workgroup
-// offsets) -> k_unlz4_ix_list (candidates in order, the rank of every bitmap word) -> k_unlz4_ix_walk
-// (each candidate's successor by rank, in parallel; then one wavefront walks the successor array 64
+// offsets) -> k_unlz4_ix_list (candidates in order, the rank of every bitmap word) -> k_unlz4_ix_link
+// (each candidate's successor by rank) -> k_unlz4_ix_walk (one wavefront walks the successor array 64
 // entries per register window, v_readlane per hop, and the workgroup writes the blocks).  Whatever the
 // candidates cannot settle -- a bad header, r0 not a candidate, a successor that is not one (a frame
 // that ends malformed), too many candidates -- falls back to the serial walk, so meta is exactly
 // unlz4_index_serial's.
-constexpr uint32_t kIxHops = 3;
-constexpr uint32_t kIxWgWords = 256;  // bitmap words (32 offsets each) per workgroup of k_unlz4_ix_cand
+constexpr uint32_t kIxHops = 5;       // a false candidate needs five words in a row that point inside the frame
+constexpr uint32_t kIxWgWords = 64;   // bitmap words (32 offsets each) per 256-thread workgroup: 8 offsets a thread
 constexpr uint32_t kIxEnd = 0xFFFFFFFFu, kIxBad = 0xFFFFFFFEu;
 
 __device__ __forceinline__ uint32_t ix_kind(const uint8_t* f, uint64_t n, const UnHeader& h, uint64_t r, uint32_t word,
@@ -810,44 +810,49 @@ __device__ __forceinline__ bool ix_candidate(const uint8_t* f, uint64_t n, const
 }
 
 // offsets b0 + 32 w + j (j < 32, b0 = r0 rounded down to 4, offsets below r0 left out) of bitmap word w;
-// the span ends at n inclusive (a legacy frame's end)
+// the span ends at n inclusive (a legacy frame's end).  Four threads per word, 8 offsets each: the rare
+// offsets whose first word points inside the frame follow their chain with dependent loads, so few offsets
+// per thread keep those waits short and many in flight
 __global__ __launch_bounds__(256) void k_unlz4_ix_cand(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
                                                        uint32_t* __restrict__ bits, uint32_t* __restrict__ wgCount)
 {
   __shared__ uint32_t s_sum[4];
   const UnHeader h = un_header(f, n);
-  const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + threadIdx.x;
+  const uint32_t tid = threadIdx.x, q = tid & 3u;
+  const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + (tid >> 2);
   uint32_t m = 0;
   if (w < nWords && h.st == 0) {
-    const uint64_t p0 = (h.r0 & ~3ull) + 32 * w;
-    const bool fast = (reinterpret_cast<uintptr_t>(f + p0) & 3u) == 0 && p0 + 40 <= n && p0 >= h.r0;
-    if (fast) {
-      // 36 bytes as nine aligned dwords: the 32 words by alignbyte, no further loads for the common BAD
-      const uint32_t* q = reinterpret_cast<const uint32_t*>(f + p0);
-      uint32_t d[9];
+    const uint64_t p0 = (h.r0 & ~3ull) + 32 * w + 8 * q;
+    if ((reinterpret_cast<uintptr_t>(f + p0) & 3u) == 0 && p0 + 16 <= n && p0 >= h.r0) {
+      // 12 bytes as three aligned dwords: the 8 words by alignbyte
+      const uint32_t* a = reinterpret_cast<const uint32_t*>(f + p0);
+      const uint32_t d0 = a[0], d1 = a[1], d2 = a[2];
 #pragma unroll
-      for (int k = 0; k < 9; k++) d[k] = q[k];
-#pragma unroll
-      for (int j = 0; j < 32; j++) {
-        const uint32_t word = (j & 3) ? __builtin_amdgcn_alignbyte(d[j / 4 + 1], d[j / 4], (uint32_t)(j & 3)) : d[j / 4];
+      for (int j = 0; j < 8; j++) {
+        const uint32_t lo = j < 4 ? d0 : d1, hi = j < 4 ? d1 : d2;
+        const uint32_t word = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
         if (ix_candidate(f, n, h, p0 + j, word)) m |= 1u << j;
       }
     } else {
-      for (int j = 0; j < 32; j++) {
+      for (int j = 0; j < 8; j++) {
         const uint64_t r = p0 + j;
         if (r > n) break;
         if (r >= h.r0 && ix_candidate(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u)) m |= 1u << j;
       }
     }
-    bits[w] = m;
   }
+  // the word from its four threads (consecutive lanes)
+  m <<= 8 * q;
+  m |= (uint32_t)__shfl_xor((int)m, 1);
+  m |= (uint32_t)__shfl_xor((int)m, 2);
+  if (w < nWords && h.st == 0 && q == 0) bits[w] = m;
   // the workgroup's candidate count
-  uint32_t c = (uint32_t)__popc(m);
+  uint32_t c = q == 0 ? (uint32_t)__popc(m) : 0u;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
-  if ((threadIdx.x & 63) == 0) s_sum[threadIdx.x >> 6] = c;
+  if ((tid & 63) == 0) s_sum[tid >> 6] = c;
   __syncthreads();
-  if (threadIdx.x == 0) wgCount[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+  if (tid == 0) wgCount[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
 }
 
 // exclusive scan of the per-workgroup counts (one workgroup); wgOff[nWg] = the number of candidates
@@ -891,7 +896,8 @@ __global__ __launch_bounds__(256) void k_unlz4_ix_list(const uint8_t* __restrict
   const UnHeader h = un_header(f, n);
   if (h.st != 0 || (uint64_t)wgOff[nWg] > cap) return;
   const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + threadIdx.x;
-  const uint32_t m = w < nWords ? bits[w] : 0u;
+  const bool mine = threadIdx.x < kIxWgWords && w < nWords;
+  const uint32_t m = mine ? bits[w] : 0u;
   const uint32_t v = (uint32_t)__popc(m), lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t x = v;
 #pragma unroll
@@ -903,12 +909,42 @@ __global__ __launch_bounds__(256) void k_unlz4_ix_list(const uint8_t* __restrict
   __syncthreads();
   uint32_t rank = wgOff[blockIdx.x] + x - v;
   for (uint32_t k = 0; k < wv; k++) rank += s_w[k];
-  if (w < nWords) wordPre[w] = rank;
+  if (mine) wordPre[w] = rank;
   uint32_t mm = m;
   while (mm) {
     const uint32_t j = (uint32_t)__builtin_ctz(mm);
     mm &= mm - 1u;
     list[rank++] = (h.r0 & ~3ull) + 32 * w + j;
+  }
+}
+
+// the rank of offset q among the candidates, or kIxBad when q is not one
+__device__ __forceinline__ uint32_t ix_rank(const UnHeader& h, uint64_t nWords, const uint32_t* __restrict__ bits,
+                                            const uint32_t* __restrict__ wordPre, uint64_t q)
+{
+  if (q < h.r0) return kIxBad;
+  const uint64_t rel = q - (h.r0 & ~3ull), w = rel >> 5;
+  if (w >= nWords) return kIxBad;
+  const uint32_t m = bits[w], b = (uint32_t)(rel & 31);
+  if (!((m >> b) & 1u)) return kIxBad;
+  return wordPre[w] + (uint32_t)__popc(m & ((1u << b) - 1u));
+}
+
+// every candidate's successor (kIxEnd: the chain ends there, kIxBad: the next offset is no candidate),
+// workgroup b taking the candidates k_unlz4_ix_list listed for its offsets
+__global__ __launch_bounds__(64) void k_unlz4_ix_link(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
+                                                      const uint32_t* __restrict__ bits, const uint32_t* __restrict__ wgOff,
+                                                      uint32_t nWg, uint64_t cap, const uint32_t* __restrict__ wordPre,
+                                                      const uint64_t* __restrict__ list, uint32_t* __restrict__ link)
+{
+  const UnHeader h = un_header(f, n);
+  if (h.st != 0 || (uint64_t)wgOff[nWg] > cap) return;
+  const uint32_t a = wgOff[blockIdx.x], b = wgOff[blockIdx.x + 1];
+  for (uint32_t i = a + threadIdx.x; i < b; i += 64) {
+    const uint64_t r = list[i];
+    uint64_t next = 0;
+    const uint32_t k = ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next);
+    link[i] = k ? k : ix_rank(h, nWords, bits, wordPre, next);
   }
 }
 
@@ -923,30 +959,12 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const UnHeader h = un_header(f, n);
   const uint64_t M = wgOff[nWg];
-  // the rank of offset q among the candidates, or kIxBad when q is not one
-  auto rank = [&](uint64_t q) -> uint32_t {
-    if (q < h.r0) return kIxBad;
-    const uint64_t rel = q - (h.r0 & ~3ull), w = rel >> 5;
-    if (w >= nWords) return kIxBad;
-    const uint32_t m = bits[w], b = (uint32_t)(rel & 31);
-    if (!((m >> b) & 1u)) return kIxBad;
-    return wordPre[w] + (uint32_t)__popc(m & ((1u << b) - 1u));
-  };
   const bool usable = h.st == 0 && M <= cap && M < (uint64_t)kIxBad;
-  // every candidate's successor (kIxEnd: the chain ends there, kIxBad: the next offset is no candidate)
-  if (usable)
-    for (uint64_t i = tid; i < M; i += 1024) {
-      const uint64_t r = list[i];
-      uint64_t next = 0;
-      const uint32_t k = ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next);
-      link[i] = k ? k : rank(next);
-    }
-  __syncthreads();
   if (tid < 64) {
     // one wavefront follows the successors from r0: 64 of them per register window, one v_readlane per
     // hop; the window's successor indices mostly lie in it or the next (prefetched) one
     uint32_t st = 1, nb = 0;
-    uint32_t i = usable ? rank(h.r0) : kIxBad;
+    uint32_t i = usable ? ix_rank(h, nWords, bits, wordPre, h.r0) : kIxBad;
     i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
     if (i != kIxBad) {
       uint64_t base = i & ~63u;
@@ -1346,7 +1364,8 @@ void launch_unlz4_index_par(const uint8_t* f, uint64_t n, void* scratch, UnBlock
   uint32_t* chain = reinterpret_cast<uint32_t*>(p + L.off[6]);
   hipLaunchKernelGGL(k_unlz4_ix_cand, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgCount);
   hipLaunchKernelGGL(k_unlz4_ix_scan, dim3(1), dim3(1024), 0, s, wgCount, nWg, wgOff);
-  hipLaunchKernelGGL(k_unlz4_ix_list, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list);
+  hipLaunchKernelGGL(k_unlz4_ix_list, dim3(nWg), dim3(64), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list);
+  hipLaunchKernelGGL(k_unlz4_ix_link, dim3(nWg), dim3(64), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list, link);
   hipLaunchKernelGGL(k_unlz4_ix_walk, dim3(1), dim3(1024), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list, link,
                      chain, blk, maxBlocks, meta);
 }
