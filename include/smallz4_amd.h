@@ -205,6 +205,9 @@ uint32_t sz4_dict_rounds(sz4_ctx* ctx);
 /* Decoder diagnostics: the pointer-jumping passes (k_unlz4_resolve, one host round trip each) the last
  * decode took in split mode (frames with blocks of >= 256 KiB payload), 0 when it decoded block by block. */
 uint32_t sz4_unlz4_resolve_passes(sz4_ctx* ctx);
+/* 1 when the last decode's block index came from the parallel index, 0 when the serial size-word walk
+ * decided (a malformed frame, too many candidates, or SZ4_UNLZ4_INDEX=0). */
+int sz4_unlz4_index_parallel(sz4_ctx* ctx);
 
 /* Last error message of the context ("" if none). */
 const char* sz4_last_error(sz4_ctx* ctx);

@@ -271,6 +271,10 @@ class Compressor:
         """Pointer-jumping passes of the last split-mode decode (0: decoded block by block)."""
         return int(self._lib.sz4_unlz4_resolve_passes(self._h))
 
+    def unlz4_index_parallel(self) -> bool:
+        """Whether the last decode's block index came from the parallel index (not the serial walk)."""
+        return bool(self._lib.sz4_unlz4_index_parallel(self._h))
+
     def set_timing(self, on: bool):
         self._lib.sz4_set_timing(self._h, int(on))
 

@@ -54,6 +54,7 @@ SIGNATURES = {
     "sz4_set_pool_cap": (None, [_u64]),
     "sz4_dict_rounds": (_u32, [_vp]),
     "sz4_unlz4_resolve_passes": (_u32, [_vp]),
+    "sz4_unlz4_index_parallel": (_i32, [_vp]),
     "sz4_last_error": (ctypes.c_char_p, [_vp]),
 }
 

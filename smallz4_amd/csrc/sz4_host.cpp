@@ -225,6 +225,7 @@ struct sz4_ctx {
   std::vector<UnSub> hSub;
   bool unSplit = false;  // the last planned frame decodes in split mode
   uint32_t unResolvePasses = 0;  // pointer-jumping passes the last split-mode decode took
+  bool unIndexParallel = false;  // the last frame index came from the parallel index (not the serial walk)
   int unSplitMode = getenv("SZ4_UNLZ4_SPLIT") ? atoi(getenv("SZ4_UNLZ4_SPLIT")) : -1;  // -1 auto, 0 never, 1 always
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
   int dictLegacy = 0;
@@ -656,7 +657,7 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
 {
   hipError_t e;
   uint64_t maxBlocks = std::min<uint64_t>(n / 5 + 2, 1u << 16);  // a block takes >= 5 frame bytes
-  uint64_t meta[3] = {0, 0, 0};
+  uint64_t meta[4] = {0, 0, 0, 0};
   for (;;) {
     if ((e = c->unBlk.reserve(maxBlocks * sizeof(UnBlock) + 64)) || (e = c->unMeta.reserve(64)))
       return c->fail(SZ4_E_NOMEM, "decoder scratch", e);
@@ -671,6 +672,7 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
     maxBlocks = n / 5 + 2;
   }
   const uint32_t nb = (uint32_t)meta[0];
+  c->unIndexParallel = meta[3] == 1;
   c->hUn.resize(nb);
   c->unSplit = false;
   // split mode needs about twice the per-block decoder's scratch (the u32 image, the sub-segment lists):
@@ -1629,6 +1631,8 @@ uint64_t sz4_device_bytes(sz4_ctx* c)
 uint32_t sz4_dict_rounds(sz4_ctx* c) { return c ? c->dictRounds : 0u; }
 
 uint32_t sz4_unlz4_resolve_passes(sz4_ctx* c) { return c && c->unSplit ? c->unResolvePasses : 0u; }
+
+int sz4_unlz4_index_parallel(sz4_ctx* c) { return c && c->unIndexParallel ? 1 : 0; }
 
 const char* sz4_last_error(sz4_ctx* c) { return c ? c->err.c_str() : "no context"; }
 

@@ -728,7 +728,8 @@ __device__ __forceinline__ UnHeader un_header(const uint8_t* f, uint64_t n)
 }
 
 // the walk in order, one lane: meta[0] = blocks found, meta[1] = 0 (frame end reached), 1 (malformed
-// after meta[0] blocks) or 2 (more than maxBlocks), meta[2] = legacy frame
+// after meta[0] blocks) or 2 (more than maxBlocks), meta[2] = legacy frame, meta[3] = 1 when the parallel
+// index decided (0: the serial walk)
 __device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk, uint64_t maxBlocks,
                                    uint64_t* __restrict__ meta)
 {
@@ -761,6 +762,7 @@ __device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, Un
   meta[0] = nb;
   meta[1] = st;
   meta[2] = h.legacy ? 1 : 0;
+  meta[3] = 0;  // the serial walk decided
 }
 
 __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
@@ -778,14 +780,15 @@ __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ 
 // must point exactly inside the frame, kIxHops times over), so the true chain is the walk from r0 over
 // the candidates: k_unlz4_ix_cand (a bit per offset, a count per workgroup) -> k_unlz4_ix_scan (workgroup
 // offsets) -> k_unlz4_ix_list (candidates in order, the rank of every bitmap word) -> k_unlz4_ix_link
-// (each candidate's successor by rank) -> k_unlz4_ix_walk (one wavefront walks the successor array 64
-// entries per register window, v_readlane per hop, and the workgroup writes the blocks).  Whatever the
+// (each candidate's successor by rank) -> k_unlz4_ix_walk (one wavefront takes the successors 64 at a time,
+// finds the path through them by binary lifting, and the workgroup writes the blocks).  Whatever the
 // candidates cannot settle -- a bad header, r0 not a candidate, a successor that is not one (a frame
 // that ends malformed), too many candidates -- falls back to the serial walk, so meta is exactly
 // unlz4_index_serial's.
 constexpr uint32_t kIxHops = 5;       // a false candidate needs five words in a row that point inside the frame
-constexpr uint32_t kIxWgWords = 64;   // bitmap words (32 offsets each) per 256-thread workgroup: 8 offsets a thread
+constexpr uint32_t kIxWgWords = 256;  // bitmap words (32 offsets each) per 1024-thread workgroup: 8 offsets a thread
 constexpr uint32_t kIxEnd = 0xFFFFFFFFu, kIxBad = 0xFFFFFFFEu;
+constexpr uint32_t kIxLds = 16384;  // successors k_unlz4_ix_walk stages in LDS (64 KiB)
 
 __device__ __forceinline__ uint32_t ix_kind(const uint8_t* f, uint64_t n, const UnHeader& h, uint64_t r, uint32_t word,
                                             uint64_t& next)
@@ -798,49 +801,66 @@ __device__ __forceinline__ uint32_t ix_kind(const uint8_t* f, uint64_t n, const 
   return r + 4 + word <= n && next <= n ? 0u : kIxBad;
 }
 
-__device__ __forceinline__ bool ix_candidate(const uint8_t* f, uint64_t n, const UnHeader& h, uint64_t r, uint32_t word)
-{
-  uint64_t next = 0;
-  uint32_t k = ix_kind(f, n, h, r, word, next);
-  for (uint32_t hop = 1; k == 0u && hop < kIxHops; hop++) {
-    r = next;
-    k = ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next);
-  }
-  return k != kIxBad;
-}
-
 // offsets b0 + 32 w + j (j < 32, b0 = r0 rounded down to 4, offsets below r0 left out) of bitmap word w;
-// the span ends at n inclusive (a legacy frame's end).  Four threads per word, 8 offsets each: the rare
-// offsets whose first word points inside the frame follow their chain with dependent loads, so few offsets
-// per thread keep those waits short and many in flight
-__global__ __launch_bounds__(256) void k_unlz4_ix_cand(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
-                                                       uint32_t* __restrict__ bits, uint32_t* __restrict__ wgCount)
+// the span ends at n inclusive (a legacy frame's end).  Four threads per word, 8 offsets each.  An END
+// offset is a candidate at once; a BLOCK offset (its word points inside the frame: a few percent of the
+// offsets of compressed data, almost none of text) follows its chain -- breadth-first over the thread's 8
+// offsets, so each hop's loads go out together and a wavefront waits once per hop, not once per offset
+__global__ __launch_bounds__(1024) void k_unlz4_ix_cand(const uint8_t* __restrict__ f, uint64_t n, uint64_t nWords,
+                                                        uint32_t* __restrict__ bits, uint32_t* __restrict__ wgCount)
 {
-  __shared__ uint32_t s_sum[4];
+  __shared__ uint32_t s_sum[16];
   const UnHeader h = un_header(f, n);
   const uint32_t tid = threadIdx.x, q = tid & 3u;
   const uint64_t w = (uint64_t)blockIdx.x * kIxWgWords + (tid >> 2);
-  uint32_t m = 0;
+  uint32_t ok = 0, live = 0;  // offset j: a candidate / its chain still to follow
+  uint64_t cur[8];
   if (w < nWords && h.st == 0) {
     const uint64_t p0 = (h.r0 & ~3ull) + 32 * w + 8 * q;
     if ((reinterpret_cast<uintptr_t>(f + p0) & 3u) == 0 && p0 + 16 <= n && p0 >= h.r0) {
-      // 12 bytes as three aligned dwords: the 8 words by alignbyte
+      // 12 bytes as three aligned dwords, the 8 words by alignbyte, the first hop in 32-bit arithmetic
       const uint32_t* a = reinterpret_cast<const uint32_t*>(f + p0);
       const uint32_t d0 = a[0], d1 = a[1], d2 = a[2];
+      const uint64_t rem64 = n - p0;
+      const uint32_t rem = rem64 > 0xFFFFFF00ull ? 0xFFFFFF00u : (uint32_t)rem64;
+      const uint32_t bs = h.blockSum ? 4u : 0u;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint32_t lo = j < 4 ? d0 : d1, hi = j < 4 ? d1 : d2;
         const uint32_t word = (j & 3) ? __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(j & 3)) : lo;
-        if (ix_candidate(f, n, h, p0 + j, word)) m |= 1u << j;
+        const uint32_t len = h.legacy ? word : word & 0x7FFFFFFFu;
+        const uint32_t room = rem - (uint32_t)j - 4u;  // rem >= 16 > j + 4
+        if (len == 0u) ok |= 1u << j;
+        else if (len <= room && len + bs <= room) live |= 1u << j;
+        cur[j] = p0 + (uint64_t)j + 4u + len + bs;
       }
     } else {
+#pragma unroll
       for (int j = 0; j < 8; j++) {
         const uint64_t r = p0 + j;
-        if (r > n) break;
-        if (r >= h.r0 && ix_candidate(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u)) m |= 1u << j;
+        uint64_t next = 0;
+        const uint32_t k = r >= h.r0 && r <= n ? ix_kind(f, n, h, r, r + 4 <= n ? un_rd32(f, n, r) : 0u, next) : kIxBad;
+        cur[j] = next;
+        if (k == kIxEnd) ok |= 1u << j;
+        else if (k == 0u) live |= 1u << j;
       }
     }
   }
+  for (uint32_t hop = 1; hop < kIxHops && __any(live != 0u); hop++) {
+    uint32_t wd[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) wd[j] = ((live >> j) & 1u) && cur[j] + 4 <= n ? un_rd32(f, n, cur[j]) : 0u;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      if ((live >> j) & 1u) {
+        uint64_t next = 0;
+        const uint32_t k = ix_kind(f, n, h, cur[j], wd[j], next);
+        cur[j] = next;
+        if (k == kIxEnd) ok |= 1u << j;
+        if (k != 0u) live &= ~(1u << j);
+      }
+  }
+  uint32_t m = ok | live;  // chains still BLOCK after kIxHops hops
   // the word from its four threads (consecutive lanes)
   m <<= 8 * q;
   m |= (uint32_t)__shfl_xor((int)m, 1);
@@ -852,7 +872,11 @@ __global__ __launch_bounds__(256) void k_unlz4_ix_cand(const uint8_t* __restrict
   for (int o = 32; o >= 1; o >>= 1) c += (uint32_t)__shfl_xor((int)c, o);
   if ((tid & 63) == 0) s_sum[tid >> 6] = c;
   __syncthreads();
-  if (tid == 0) wgCount[blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+  if (tid == 0) {
+    uint32_t t = 0;
+    for (int k = 0; k < 16; k++) t += s_sum[k];
+    wgCount[blockIdx.x] = t;
+  }
 }
 
 // exclusive scan of the per-workgroup counts (one workgroup); wgOff[nWg] = the number of candidates
@@ -956,51 +980,64 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
                                                         uint64_t maxBlocks, uint64_t* __restrict__ meta)
 {
   __shared__ uint32_t s_nb, s_st;
+  __shared__ uint32_t s_link[kIxLds];  // the successors, when they fit: the walk then reads no HBM
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const UnHeader h = un_header(f, n);
   const uint64_t M = wgOff[nWg];
   const bool usable = h.st == 0 && M <= cap && M < (uint64_t)kIxBad;
+  const bool inLds = usable && M <= kIxLds;
+  if (inLds)
+    for (uint32_t i = tid; i < (uint32_t)M; i += 1024) s_link[i] = link[i];
+  __syncthreads();
   if (tid < 64) {
-    // one wavefront follows the successors from r0: 64 of them per register window, one v_readlane per
-    // hop; the window's successor indices mostly lie in it or the next (prefetched) one
+    // one wavefront follows the successors from r0, 64 candidates per step: lane l holds candidate e + l
+    // (e: the entry), its local successor in the window (64: it leaves the window, ends or is BAD), the
+    // doubling tables J1..J32 by ds_bpermute, and every lane finds the last path node at or below itself by
+    // binary lifting from lane 0 -- the lanes that find themselves are the path (as k_walk does for the
+    // parse).  The path's last node leads to the next window's entry.
     uint32_t st = 1, nb = 0;
-    uint32_t i = usable ? ix_rank(h, nWords, bits, wordPre, h.r0) : kIxBad;
-    i = (uint32_t)__builtin_amdgcn_readfirstlane((int)i);
-    if (i != kIxBad) {
-      uint64_t base = i & ~63u;
-      uint32_t cur = base + lane < M ? link[base + lane] : kIxBad;
-      uint32_t nxt = base + 64 + lane < M ? link[base + 64 + lane] : kIxBad;
-      uint32_t rec = 0;  // the chain's ranks, 64 per vector store
-      for (;;) {
-        if ((uint64_t)i >= base + 64) {
-          if ((uint64_t)i < base + 128) {
-            base += 64;
-            cur = nxt;
-          } else {
-            base = i & ~63u;
-            cur = base + lane < M ? link[base + lane] : kIxBad;
-          }
-          nxt = base + 64 + lane < M ? link[base + 64 + lane] : kIxBad;
-        }
-        const uint32_t l = un_rdlane(cur, (uint32_t)(i - base));
-        if (l == kIxEnd) {
-          st = 0;
-          break;
-        }
-        if (l == kIxBad) break;  // the serial walk decides
-        if (nb == maxBlocks) {
-          st = 2;
-          break;
-        }
-        rec = un_wrlane(rec, i, nb & 63u);
-        nb++;
-        if ((nb & 63u) == 0) chain[nb - 64 + lane] = rec;
-        i = l;
+    uint32_t e = usable ? ix_rank(h, nWords, bits, wordPre, h.r0) : kIxBad;
+    e = (uint32_t)__builtin_amdgcn_readfirstlane((int)e);
+    // table T at per-lane index x (x = 64: "outside", stays 64)
+    auto at = [&](uint32_t T, uint32_t x) -> uint32_t {
+      const uint32_t r = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x < 64u ? x : 63u) << 2), (int)T);
+      return x < 64u ? r : 64u;
+    };
+    while (e != kIxBad) {
+      const uint64_t ci = (uint64_t)e + lane;
+      const uint32_t val = ci < M ? (inLds ? s_link[ci] : link[ci]) : kIxBad;
+      const uint32_t nl = val < (uint32_t)M && (uint64_t)val < (uint64_t)e + 64 ? val - e : 64u;
+      uint32_t J[6];
+      J[0] = nl;
+#pragma unroll
+      for (int k = 1; k < 6; k++) J[k] = at(J[k - 1], J[k - 1]);
+      uint32_t pos = 0;
+#pragma unroll
+      for (int k = 5; k >= 0; k--) {
+        const uint32_t c = at(J[k], pos);
+        if (c <= lane) pos = c;
       }
-      if (nb & 63u) {
-        const uint32_t b0 = nb & ~63u;
-        if (lane < (nb & 63u)) chain[b0 + lane] = rec;
+      const uint64_t path = __ballot(pos == lane);  // lane 0 is on it
+      const uint32_t last = 63u - (uint32_t)__builtin_clzll(path);
+      const uint32_t exitv = un_rdlane(val, last);
+      // the path's nodes are blocks, except a last node that ends the chain (END) or cannot be followed (BAD)
+      const uint64_t blocks = exitv == kIxEnd || exitv == kIxBad ? path & ~(1ull << last) : path;
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(blocks);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(blocks >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)blocks, 0u));
+      const bool take = ((blocks >> lane) & 1ull) && (uint64_t)nb + below < maxBlocks;
+      if (take) chain[nb + below] = e + lane;
+      if ((uint64_t)nb + cnt > maxBlocks) {
+        nb = (uint32_t)maxBlocks;
+        st = 2;
+        break;
       }
+      nb += cnt;
+      if (exitv == kIxEnd) {
+        st = 0;
+        break;
+      }
+      if (exitv == kIxBad) break;  // the serial walk decides
+      e = exitv;  // >= e + 64: the next window
     }
     if (lane == 0) {
       s_nb = nb;
@@ -1030,6 +1067,7 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
     meta[0] = nb;
     meta[1] = st;
     meta[2] = h.legacy ? 1 : 0;
+    meta[3] = 1;  // the parallel index decided
   }
 }
 
@@ -1362,9 +1400,9 @@ void launch_unlz4_index_par(const uint8_t* f, uint64_t n, void* scratch, UnBlock
   uint64_t* list = reinterpret_cast<uint64_t*>(p + L.off[4]);
   uint32_t* link = reinterpret_cast<uint32_t*>(p + L.off[5]);
   uint32_t* chain = reinterpret_cast<uint32_t*>(p + L.off[6]);
-  hipLaunchKernelGGL(k_unlz4_ix_cand, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgCount);
+  hipLaunchKernelGGL(k_unlz4_ix_cand, dim3(nWg), dim3(1024), 0, s, f, n, words, bits, wgCount);
   hipLaunchKernelGGL(k_unlz4_ix_scan, dim3(1), dim3(1024), 0, s, wgCount, nWg, wgOff);
-  hipLaunchKernelGGL(k_unlz4_ix_list, dim3(nWg), dim3(64), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list);
+  hipLaunchKernelGGL(k_unlz4_ix_list, dim3(nWg), dim3(256), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list);
   hipLaunchKernelGGL(k_unlz4_ix_link, dim3(nWg), dim3(64), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list, link);
   hipLaunchKernelGGL(k_unlz4_ix_walk, dim3(1), dim3(1024), 0, s, f, n, words, bits, wgOff, nWg, cap, wordPre, list, link,
                      chain, blk, maxBlocks, meta);

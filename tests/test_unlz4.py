@@ -168,6 +168,7 @@ def test_unlz4_device_api_roundtrip_100mb(compressor):
     out = torch.empty(len(data), dtype=torch.uint8, device="cuda")
     n = compressor.unlz4_device(f.data_ptr(), len(frame), out.data_ptr(), len(data))
     assert n == len(data) and torch.equal(out, t)
+    assert compressor.unlz4_index_parallel()  # 1526 blocks indexed without the serial walk
     with pytest.raises(NativeError):
         compressor.unlz4_device(f.data_ptr(), len(frame), out.data_ptr(), len(data) - 1)
 
@@ -279,6 +280,7 @@ def test_unlz4_index_false_candidates(compressor):
     for frame in (compressor.compress_blocks(payload, 65536, 0), compressor.compress_blocks(payload, 4099, 0),
                   compressor.lz4(payload, 1, b"", True), compressor.lz4(payload, 0)):
         assert check(compressor, frame) == payload
+        assert compressor.unlz4_index_parallel()
     # truncated and bit-flipped outer frames: the index decides exactly as the one-lane walk
     frame = compressor.compress_blocks(payload, 65536, 0)
     for k in (7, 11, 65540 + 11, len(frame) // 2, len(frame) - 5, len(frame) - 1):
