@@ -454,6 +454,12 @@ constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survive
 #ifndef SZ4_RUN_PREFIX
 #define SZ4_RUN_PREFIX 1  // 0: k_find extends candidates inside a same-letter run byte by byte (A/B)
 #endif
+#ifndef SZ4_BIG_INV
+#define SZ4_BIG_INV 1  // 0: k_find_big finds a run piece's place in its bucket by binary search (A/B)
+#endif
+#ifndef SZ4_LPF_BLOCK_MIN
+#define SZ4_LPF_BLOCK_MIN 65536  // LPF targets go to k_find_big only in blocks larger than this (A/B)
+#endif
 #ifndef SZ4_HIT2
 #define SZ4_HIT2 1  // 0: round 3's filter-hit code (masks from need bytes, satOk applied afterwards)
 #endif
@@ -1088,7 +1094,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     const uint64_t predLoF = S.w0 > B.low ? S.w0 : B.low;
     // LPF targets in blocks above 64 KiB only: a 64 KiB block's groups are small, and text gains nothing
     // there that would pay for k_find_big's pass over the segment
-    const bool lpfBlock = B.end - B.start > 65536u;
+    const bool lpfBlock = B.end - B.start > (uint64_t)SZ4_LPF_BLOCK_MIN;
 #if SZ4_LPF_LOCAL
     // the LPF decision from the chunk itself: a target of the group that began before the chunk (more than
     // kLpfMin members below it) whose preceding byte at least 3/4 of that group's lanes in the chunk share
@@ -3179,6 +3185,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       if (tid == 0 && !s_mixed && nRuns > (uint32_t)(S.s1 - S.s0)) SZ4_D6C(18, 1);
 #endif
       if (!s_mixed && nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
+      // with at most half as many pieces, BK's upper half maps a piece to its place in its bucket
+      const bool invBk = SZ4_BIG_INV && nRuns <= nTg / 2;
       // B. buckets by next byte
       for (uint32_t k = tid; k < nRuns; k += kFindThreads) atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u);
       __syncthreads();
@@ -3208,7 +3216,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
             const uint32_t al = rdlane(a, l);
             const uint64_t m = __ballot(a == al);
             const uint32_t at = s_cur[0][al];
-            if (a == al) BK[at + (uint32_t)__builtin_popcountll(m & below)] = k;
+            if (a == al) {
+              const uint32_t q = at + (uint32_t)__builtin_popcountll(m & below);
+              BK[q] = k;
+              if (invBk) BK[nTg / 2 + k] = q;  // the piece's place in its bucket
+            }
             if (lane == 0) s_cur[0][al] = at + (uint32_t)__builtin_popcountll(m);
             rest &= ~m;
           }
@@ -3264,15 +3276,24 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
           if (Rp >= limit || ai == kAEnd) return;
           const uint32_t b0 = s_cls[ai];
           uint32_t bLo = b0, bHi = s_cls[ai + 1];  // p's piece in it
-          while (bLo < bHi) {
-            const uint32_t mid = (bLo + bHi) >> 1;
-            if (BK[mid] < lo) bLo = mid + 1;
-            else bHi = mid;
+          if (invBk) {
+            bLo = BK[nTg / 2 + lo];
+          } else {
+            while (bLo < bHi) {
+              const uint32_t mid = (bLo + bHi) >> 1;
+              if (BK[mid] < lo) bLo = mid + 1;
+              else bHi = mid;
+            }
           }
+          // the next piece index is loaded while this one's piece is read (clamped, unconditional)
+          uint32_t jNext = BK[bLo > b0 ? bLo - 1u : b0];
           for (uint32_t b = bLo; b-- > b0;) {
             SZ4_D6C(9, 1);
+            uint32_t j;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(j) : "v"(jNext));
+            jNext = BK[b > b0 ? b - 1u : b0];
             uint32_t fj, ej, lj;
-            piece(BK[b], fj, ej, lj);
+            piece(j, fj, ej, lj);
             if (lj < lbRel) break;     // it and every earlier piece lie below the window
             const uint32_t c = ej - Rp;  // its position with R(c) = Rp
             if (c < fj || c > lj || c < lbRel) continue;
@@ -3492,15 +3513,26 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
         m2 = (uint32_t)(mk >> 32);
       };
 #endif
-      for (int part = 0; part < 2; part++) {
-        const uint32_t lo = part == 0 ? r0a : r1a, hi = part == 0 ? r0b : r1b;
-        for (uint32_t base = lo; base < hi; base += 64) {
-          const uint32_t ci = base + lane;
-          const uint32_t ce = ci < hi ? C[ci] : 0xFFFFFFFFu;
+      {
+        // both candidate ranges as one sequence, 64 per step; the next step's entries of C are loaded
+        // while this step's are scanned (unconditionally, at a clamped index: a load under a branch would
+        // be waited for at once)
+        const uint32_t len0 = r0b - r0a, tot = len0 + (r1b - r1a);
+        auto cidx = [&](uint32_t j) -> uint32_t {
+          const uint32_t jj = j < tot ? j : (tot ? tot - 1u : 0u);
+          return jj < len0 ? r0a + jj : r1a + (jj - len0);
+        };
+        uint32_t ceNext = tot ? C[cidx(lane)] : 0u;
+        for (uint32_t base = 0; base < tot; base += 64) {
+          uint32_t ce;
+          asm volatile("v_mov_b32 %0, %1" : "=v"(ce) : "v"(ceNext));
+          ceNext = C[cidx(base + 64u + lane)];
+          const bool inR = base + lane < tot;
+          ce = inR ? ce : 0xFFFFFFFFu;
           const uint32_t cr = ce & 0x1FFFFu;
-          const uint64_t cp = S.w0 + (ci < hi ? cr : 0u);
+          const uint64_t cp = S.w0 + (inR ? cr : 0u);
           const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
-          const uint32_t n = hi - base < 64u ? hi - base : 64u;
+          const uint32_t n = tot - base < 64u ? tot - base : 64u;
 #if SZ4_BCAST_DPP
           // 16 candidates per register, every row a copy; step K takes candidate q0 + K to every lane by DPP
           // row_newbcast:K (VGPR operands only), the exact prefix only when the filter lets it through
