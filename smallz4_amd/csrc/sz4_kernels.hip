@@ -1686,10 +1686,11 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #if SZ4_DIAG == 3
           dL++;
 #endif
-          rRel = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rRel, kWaveShr1, 0xF, 0xF, false);
-          r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
-          r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
-          r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
+          // (bound_ctrl: lane 0 receives 0 without an old value to set up)
+          rRel = (uint32_t)__builtin_amdgcn_mov_dpp((int)rRel, kWaveShr1, 0xF, 0xF, true);
+          r0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r0, kWaveShr1, 0xF, 0xF, true);
+          r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r1, kWaveShr1, 0xF, 0xF, true);
+          r2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r2, kWaveShr1, 0xF, 0xF, true);
           cl--;
           if (walk) {
             if (needWin && rRel < lbRel) run = false;
@@ -1716,6 +1717,48 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
           int32_t k = 0;
+#if SZ4_BCAST_DPP
+          {
+            // as at -9: 16 candidates per register, every row a copy, candidate q0 + K to every lane by DPP
+            // row_newbcast:K folded into the xor -- in order, nearest first, as the step count needs; with a
+            // window test, a lane takes the first kc candidates of the block (positions descend with k)
+            uint32_t kc = (uint32_t)n;
+            if (needWin) {
+              uint32_t a = 0, b = (uint32_t)n;
+#pragma unroll
+              for (int it = 0; it < 7; it++) {
+                const uint32_t mid = (a + b) >> 1;
+                const uint32_t fk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mid << 2), (int)fRel);
+                const bool go = a < b;
+                if (go && fk >= lbRel) a = mid + 1u;
+                else if (go) b = mid;
+              }
+              kc = a;
+            }
+            for (int32_t q0 = 0; q0 < n && __ballot(run); q0 += 16) {
+              const int srcl = (int)((uint32_t)(q0 + (int32_t)(lane & 15u)) << 2);
+              const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)f0);
+              const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)f1);
+              const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)f2);
+              const int32_t cnt = n - q0 < 16 ? n - q0 : 16;
+              const uint32_t kcRel = kc > (uint32_t)q0 ? kc - (uint32_t)q0 : 0u;
+#define SZ4_BSTEP_B(K)                                                                                          \
+              if ((K) < cnt) {                                                                                  \
+                const uint32_t x0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g0, 0x150 + (K), 0xF, 0xF, true) ^ me0; \
+                const uint32_t x1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g1, 0x150 + (K), 0xF, 0xF, true) ^ me1; \
+                const uint32_t x2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)g2, 0x150 + (K), 0xF, 0xF, true) ^ me2; \
+                const bool h = run && (K) < kcRel && (x0 | (x1 & m1) | (x2 & m2)) == 0u;                          \
+                if (__ballot(h) && h) improve(S.w0 + rdlane(fRel, (uint32_t)(q0 + (K))), x1 ^ me1, x2 ^ me2);    \
+              }
+              SZ4_BSTEP_B(0) SZ4_BSTEP_B(1) SZ4_BSTEP_B(2) SZ4_BSTEP_B(3) SZ4_BSTEP_B(4) SZ4_BSTEP_B(5)
+              SZ4_BSTEP_B(6) SZ4_BSTEP_B(7) SZ4_BSTEP_B(8) SZ4_BSTEP_B(9) SZ4_BSTEP_B(10) SZ4_BSTEP_B(11)
+              SZ4_BSTEP_B(12) SZ4_BSTEP_B(13) SZ4_BSTEP_B(14) SZ4_BSTEP_B(15)
+#undef SZ4_BSTEP_B
+            }
+            if (kc < (uint32_t)n) run = false;
+            k = n;
+          }
+#endif
           if (!needWin) {
             for (; k + 4 <= n; k += 4) {
 #if SZ4_DIAG == 3
