@@ -293,23 +293,37 @@ def pmc_traffic(cfg):
 
 
 def valu_ceiling():
-    """(source, VALU instructions per SIMD per cycle at CLOCK_GHZ) sustained by tools/valu_ceiling.hip
-    (independent v_add/v_xor chains, 32 waves per CU) on the MI355X, from profiles/valu_ceiling_*.json."""
+    """The integer VALU issue rate the MI355X sustains (tools/valu_ceiling.hip, every SIMD at 8 waves,
+    independent add/xor chains, the clock read in the same run from s_memtime against s_memrealtime), from
+    the newest profiles/valu_ceiling_*.json: {"source", "vgpr": per SIMD-cycle at its measured clock with
+    VGPR operands (the shift-register and DPP tests), "sgpr": the same with SGPR operands (readlane
+    broadcasts), "clock_ghz"}.  Round 4's record (no clock, one variant) is read at CLOCK_GHZ."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "valu_ceiling_*.json")))
     if not paths:
         return None
-    best = 0.0
+    recs = []
     with open(paths[-1]) as f:
         for line in f:
             try:
-                rec = json.loads(line)
+                recs.append(json.loads(line))
             except ValueError:
                 continue
-            if rec.get("variant") == "add_xor":
-                best = max(best, rec["valu_instr_per_s"])
+    out = {"source": os.path.relpath(paths[-1], ROOT)}
+    full = [r for r in recs if r.get("waves_per_simd") == 8 and "per_simd_per_cycle" in r]
+    if full:
+        vg = [r for r in full if "vgpr" in r["variant"] or "4chains" in r["variant"]]
+        sg = [r for r in full if r["variant"] in ("add_xor_8chains", "add_16chains")]
+        if vg:
+            best = max(vg, key=lambda r: r["per_simd_per_cycle"])
+            out.update({"vgpr": best["per_simd_per_cycle"], "clock_ghz": best["clock_ghz_median"], "variant": best["variant"]})
+        if sg:
+            out["sgpr"] = max(r["per_simd_per_cycle"] for r in sg)
+        return out if "vgpr" in out else None
+    best = max((r["valu_instr_per_s"] for r in recs if r.get("variant") == "add_xor"), default=0.0)
     if not best:
         return None
-    return os.path.relpath(paths[-1], ROOT), round(best / 1024 / (CLOCK_GHZ * 1e9), 4)
+    out.update({"vgpr": round(best / 1024 / (CLOCK_GHZ * 1e9), 4), "clock_ghz": CLOCK_GHZ, "variant": "add_xor"})
+    return out
 
 
 def spawn_ranks(args):
@@ -693,10 +707,15 @@ def main():
                               "valu_frac": round(rec_p["valu_per_simd_cycle"] / 0.5, 4)})
                 ceil = valu_ceiling()
                 if ceil:
-                    # the integer VALU rate the chip sustains (tools/valu_ceiling.hip), in the same units
-                    issue.update({"valu_ceiling_measured": ceil[1],
-                                  "valu_frac_of_measured": round(rec_p["valu_per_simd_cycle"] / ceil[1], 4),
-                                  "valu_ceiling_source": ceil[0]})
+                    # the integer VALU rate the chip sustains (tools/valu_ceiling.hip), both at the clocks
+                    # measured while each ran (the kernel's from its SQ pass: GRBM_GUI_ACTIVE over the time)
+                    mine = rec_p.get("valu_per_simd_cycle_at_clock", rec_p["valu_per_simd_cycle"])
+                    issue.update({"valu_per_simd_cycle_at_clock": mine,
+                                  "clock_ghz_measured": rec_p.get("clock_ghz_measured"),
+                                  "valu_ceiling_measured": ceil["vgpr"], "valu_ceiling_clock_ghz": ceil["clock_ghz"],
+                                  "valu_ceiling_sgpr_operands": ceil.get("sgpr"),
+                                  "valu_frac_of_measured": round(mine / ceil["vgpr"], 4),
+                                  "valu_ceiling_source": ceil["source"]})
             if rec_p.get("salu_per_cu_cycle") is not None:
                 issue.update({"salu_per_cu_cycle": rec_p["salu_per_cu_cycle"], "salu_peak": 1.0,
                               "salu_frac": round(rec_p["salu_per_cu_cycle"], 4)})

@@ -32,6 +32,9 @@ namespace {
 
 constexpr uint64_t kPad = 64;                 // bytes of slack after every staged input
 constexpr uint64_t kSegTargets = 65536;       // target positions per segment
+// batch API pieces: 1 GiB of input (36-60 GB of scratch, sized for the MI355X's 288 GB): at 256 KiB
+// blocks a piece is 4096 blocks, four of the per-block repair wavefronts per SIMD instead of one
+constexpr uint64_t kBatchChunkDefault = 1ull << 30;
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
 // dictionary rounds before the in-order replay takes the chunk: each round settles at least one more
 // shortcut interval of every block, so a chunk needs at most (intervals per block) + 1 rounds, and a block
@@ -208,7 +211,7 @@ struct sz4_ctx {
   DevBuf stagedS[2];           // stream path: two chunks' staged input (chunk i+1 uploads while chunk i computes)
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
-  uint64_t batchChunk = 256ull << 20;  // sz4_compress_blocks_device: input bytes per internal pipeline run
+  uint64_t batchChunk = kBatchChunkDefault;  // sz4_compress_blocks_device: input bytes per internal pipeline run
   bool batchChunked = false;           // the last sz4_compress_blocks_device call ran in several pieces
   uint64_t streamPlanKey[5] = {~0ull, 0, 0, 0, 0};  // stream path: the chunk shape the current plan is for
   // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
@@ -1283,6 +1286,16 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   c->device = device;
   const char* sep = getenv("SZ4_SEPARATE_SORT");
   c->separateSort = sep && sep[0] == '1';
+  // tuning knobs (A/B): the batch API's piece size and the stream path's chunk size in bytes
+  // (sz4_set_batch_chunk / sz4_set_stream_chunk set them per context)
+  if (const char* bc = getenv("SZ4_BATCH_CHUNK")) {
+    const uint64_t v = strtoull(bc, nullptr, 10);
+    if (v >= (1u << 20)) c->batchChunk = v;
+  }
+  if (const char* sc = getenv("SZ4_STREAM_CHUNK")) {
+    const uint64_t v = strtoull(sc, nullptr, 10);
+    if (v >= (1u << 20)) c->streamChunk = v;
+  }
   for (auto& e : c->ev) hipEventCreate(&e);
   c->budget.bufs = c->all_buffers();
   for (DevBuf* b : c->budget.bufs) b->bud = &c->budget;
@@ -1425,7 +1438,10 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   }
   // bounded memory: whole blocks in pieces of at most batchChunk input bytes, one pipeline run each
   // (the scratch is ~60-75 bytes per input byte), written one after the other into d_out
-  const uint64_t piece = std::max<uint64_t>(block_size, c->batchChunk / block_size * block_size);
+  // under a device bound the pieces shrink with it (the scratch is 36-60 bytes per piece byte)
+  uint64_t chunk = c->batchChunk;
+  if (c->budget.limit) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(16ull << 20, c->budget.limit / 64));
+  const uint64_t piece = std::max<uint64_t>(block_size, chunk / block_size * block_size);
   float stageSum[kStages] = {};
   uint64_t pos = 0;
   if (n > piece) c->hostBytes.clear();
@@ -1529,7 +1545,7 @@ void sz4_set_stream_chunk(sz4_ctx* c, uint64_t bytes)
 
 void sz4_set_batch_chunk(sz4_ctx* c, uint64_t bytes)
 {
-  if (c) c->batchChunk = bytes ? bytes : (256ull << 20);
+  if (c) c->batchChunk = bytes ? bytes : kBatchChunkDefault;
 }
 
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)

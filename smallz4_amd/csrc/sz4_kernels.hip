@@ -5229,6 +5229,11 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
   const Block B = blocks[bIdx];
   if (B.dpCount <= 1) return;
   const uint32_t lane = threadIdx.x;
+#if SZ4_DIAG == 7
+  // k_dp_fix<false> per block: serial positions, closed-form chunks, literal chunks, segments walked
+  uint64_t d7Serial = 0, d7Closed = 0, d7Lit = 0, d7Segs = 0;
+  const uint64_t d7t0 = __builtin_readcyclecounter();
+#endif
   if constexpr (kPar) {
     // a segment without any match cannot converge (that needs a match): nothing written, k_dp_fix<false>
     // repairs it in closed form
@@ -5431,7 +5436,13 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         lowW = cl;
       }
       closedRun = false;
+#if SZ4_DIAG == 7
+      if (h == hi) d7Segs++;
+#endif
       if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
+#if SZ4_DIAG == 7
+        d7Lit++;
+#endif
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
         auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
           const uint32_t run = lits + t + 1u;
@@ -5487,6 +5498,9 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                    return false;
                  }()) {
         const uint32_t cT = closedCost + len_extra((uint32_t)(closedE - ip));
+#if SZ4_DIAG == 7
+        d7Closed++;
+#endif
         if (closedE > maxReach) maxReach = closedE;
         if (closedE != chain.E) chain.valid = chain.pending = false;
         const uint32_t delta = cT - cC;
@@ -5533,6 +5547,9 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       for (uint32_t t = 0; t < 64; t++) {
         const int32_t i = h - (int32_t)t;
         if (i < lo) break;
+#if SZ4_DIAG == 7
+        d7Serial++;
+#endif
         const uint32_t Lk = rdlane(cL, t), Dk = rdlane(cD, t);
         if (Lk >= (uint32_t)kMinMatch && i + (int32_t)Lk > maxReach) maxReach = i + (int32_t)Lk;
         lits++;
@@ -5653,6 +5670,20 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
       prevKeyLim = convBlk[k];
     }
   }
+#if SZ4_DIAG == 7
+  if (!kPar && lane == 0) {
+    const uint64_t dt = __builtin_readcyclecounter() - d7t0;
+    atomicAdd((unsigned long long*)&sz4_diag[0], (unsigned long long)d7Serial);
+    atomicAdd((unsigned long long*)&sz4_diag[1], (unsigned long long)d7Closed);
+    atomicAdd((unsigned long long*)&sz4_diag[2], (unsigned long long)d7Lit);
+    atomicAdd((unsigned long long*)&sz4_diag[3], (unsigned long long)d7Segs);
+    atomicMax((unsigned long long*)&sz4_diag[4], (unsigned long long)d7Serial);
+    atomicAdd((unsigned long long*)&sz4_diag[5], (unsigned long long)dt);
+    atomicMax((unsigned long long*)&sz4_diag[6], (unsigned long long)dt);
+    atomicAdd((unsigned long long*)&sz4_diag[7], 1ull);
+    if (rmq) atomicAdd((unsigned long long*)&sz4_diag[8], 1ull);
+  }
+#endif
 }
 
 // ================================================================================================

@@ -99,13 +99,15 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     # HBM footprint of the context for this slice (grow-only scratch)
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
-    # bounded: sz4_compress_blocks_device runs 256 MiB pieces (~60-75 B of scratch per piece byte)
-    assert footprint < 24 << 30
+    # bounded: sz4_compress_blocks_device runs pieces of 1 GiB (round 5; ~36-60 B of scratch per piece byte,
+    # plus what earlier tests left in the shared context), whatever the slice's length
+    assert footprint < 72 << 30
 
 
 def _batch_4gib(compressor, torch):
     """4 GiB of configs[4]'s shape (zeros/urandom runs, 256 KiB blocks) in ONE sz4_compress_blocks_device
-    call: the context's scratch stays under 24 GiB (the call runs 256 MiB pieces), the frame decodes
+    call: the context's scratch stays under 24 GiB (under the bound the call runs pieces of about 1/64 of it,
+    384 MiB), the frame decodes
     back on the device, every size word walks, and sampled blocks equal the reference's.  Run by
     tests/test_memory.py on the shared session context under a 24 GiB device bound."""
     bs = 262144

@@ -18,22 +18,26 @@ from smallz4_amd import synth  # noqa: E402
 
 def main():
     mb = float(sys.argv[1]) if len(sys.argv) > 1 else 64
+    workload = sys.argv[2] if len(sys.argv) > 2 else "silesia"
     n = int(mb * 1e6)
-    data = synth.silesia_like(n, workers=8)
+    if workload == "zu":  # configs[4]: zeros/urandom at 256 KiB blocks
+        data, bs = synth.zeros_urandom_range(0, n, seed=10), 262144
+    else:
+        data, bs = synth.silesia_like(n, workers=8), 4 << 20
     comp = smallz4_amd.Compressor()
     lib = comp._lib
     lib.sz4_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-    comp.compress_blocks(data, 4 << 20, 65535)
+    comp.compress_blocks(data, bs, 65535)
     assert lib.sz4_diag_clear() == 0
     comp.set_timing(True)
-    comp.compress_blocks(data, 4 << 20, 65535)
+    comp.compress_blocks(data, bs, 65535)
     st = comp.last_stage_ms()
     buf = np.zeros(32, dtype=np.uint64)
     assert lib.sz4_diag_read(buf.ctypes.data, buf.size) == 0
     names = {0: "groups found", 1: "window load", 6: "run group: entry", 2: "run group: pieces", 3: "run group: buckets",
              5: "run group: search", 7: "class path", 4: "after the groups"}
     tot = sum(int(buf[k]) for k in names)
-    print(f"{mb:.0f} MB Silesia-shaped, 4 MiB blocks, -9: stages {st}")
+    print(f"{mb:.0f} MB {workload}, {bs >> 10} KiB blocks, -9: stages {st}")
     for k, name in names.items():
         print(f"  tick[{k}] {name:22s} {int(buf[k]):.4g} ({100.0 * int(buf[k]) / max(tot, 1):.1f} %)")
     cnt = {8: "run targets", 9: "same-R piece visits", 10: "c10", 11: "c11", 12: "pieces", 13: "class groups",

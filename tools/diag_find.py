@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Diagnostic: k_find_sorted's per-wavefront counters from a SZ4_DIAG=3 build of the library
+"""Diagnostic (python3 tools/diag_find.py MB [max_chain] [enwik8|zu|silesia]): k_find_sorted's per-wavefront counters from a SZ4_DIAG=3 build of the library
 (smallz4_amd/lib/libsmallz4_amd_diag.so, built by tools/build_diag.sh): below-chunk candidate steps
 (dB), shift-register steps (dL), improve calls (dBi), extension steps (dLi) and cycles per wave."""
 import ctypes
@@ -17,16 +17,22 @@ from smallz4_amd import synth  # noqa: E402
 
 mb = float(sys.argv[1]) if len(sys.argv) > 1 else 100
 chain = int(sys.argv[2]) if len(sys.argv) > 2 else 65535
+workload = sys.argv[3] if len(sys.argv) > 3 else "enwik8"
 n = int(mb * 1e6)
-data = synth.enwik8_like(n, seed=8)
+if workload == "zu":  # configs[4]: zeros/urandom at 256 KiB blocks
+    data, bs = synth.zeros_urandom_range(0, n, seed=10), 262144
+elif workload == "silesia":  # configs[2] at 4 MiB blocks
+    data, bs = synth.silesia_like(n, seed=2), 4 << 20
+else:
+    data, bs = synth.enwik8_like(n, seed=8), 65536
 comp = smallz4_amd.Compressor()
-comp.compress_blocks(data[:1 << 20], 65536, chain)
+comp.compress_blocks(data[:1 << 22], bs, chain)
 comp.set_timing(True)
-comp.compress_blocks(data, 65536, chain)
+comp.compress_blocks(data, bs, chain)
 find_ms = comp.last_stage_ms()['find_sorted']
 lib = comp._lib
 lib.sz4_diag_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
-nwaves = ((n + 65535) // 65536) * 16
+nwaves = min((n + 65535) // 65536, 1 << 17) * 16  # 16 waves per 64 Ki-target segment
 buf = np.zeros(nwaves * 8, dtype=np.uint64)
 assert lib.sz4_diag_read(buf.ctypes.data, buf.size) == 0
 d = buf.reshape(-1, 8).astype(np.float64)
