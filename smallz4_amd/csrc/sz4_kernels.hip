@@ -1900,8 +1900,12 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(SZ4
   find_sorted_body<false>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
 }
 
+// (SZ4_FIND2_OCC: two workgroups per CU when the window fits LDS -- <= 64 VGPRs, <= 80 SGPRs)
+#ifndef SZ4_FIND2_OCC
+#define SZ4_FIND2_OCC 1
+#endif
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ4_FIND2_OCC ? 8 : 1), amdgpu_num_sgpr(SZ4_FIND2_OCC ? 80 : 102))) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                        const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                        const uint32_t* __restrict__ rankAll, uint32_t maxChain,
