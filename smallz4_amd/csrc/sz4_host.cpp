@@ -660,7 +660,7 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
 {
   hipError_t e;
   uint64_t maxBlocks = std::min<uint64_t>(n / 5 + 2, 1u << 16);  // a block takes >= 5 frame bytes
-  uint64_t meta[4] = {0, 0, 0, 0};
+  uint64_t meta[5] = {0, 0, 0, 0, 0};
   for (;;) {
     if ((e = c->unBlk.reserve(maxBlocks * sizeof(UnBlock) + 64)) || (e = c->unMeta.reserve(64)))
       return c->fail(SZ4_E_NOMEM, "decoder scratch", e);
@@ -689,13 +689,13 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
     return r;
   };
   if (nb) {
-    if ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
-        (e = hipStreamSynchronize(s)))
-      return c->fail(SZ4_E_DEVICE, "frame index", e);
-    // split mode when a block is large (one wavefront per block would leave most of the chip idle)
-    uint32_t maxLen = 0;
-    for (const UnBlock& b : c->hUn) maxLen = std::max(maxLen, b.len);
+    // split mode when a block is large (one wavefront per block would leave most of the chip idle); the
+    // index reports the longest payload, so block-wise decoding reads the records back only after sizes
+    const uint64_t maxLen = meta[4];
     c->unSplit = c->unSplitMode == 1 || (c->unSplitMode != 0 && maxLen >= kUnSplitMin);
+    if (c->unSplit && ((e = hipMemcpyAsync(c->hUn.data(), c->unBlk.p, nb * sizeof(UnBlock), hipMemcpyDeviceToHost, s)) ||
+                       (e = hipStreamSynchronize(s))))
+      return c->fail(SZ4_E_DEVICE, "frame index", e);
   }
   if (nb && c->unSplit) {
     c->hSub.clear();

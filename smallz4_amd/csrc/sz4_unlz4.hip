@@ -729,12 +729,12 @@ __device__ __forceinline__ UnHeader un_header(const uint8_t* f, uint64_t n)
 
 // the walk in order, one lane: meta[0] = blocks found, meta[1] = 0 (frame end reached), 1 (malformed
 // after meta[0] blocks) or 2 (more than maxBlocks), meta[2] = legacy frame, meta[3] = 1 when the parallel
-// index decided (0: the serial walk)
+// index decided (0: the serial walk), meta[4] = the longest payload (the host's split decision)
 __device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk, uint64_t maxBlocks,
                                    uint64_t* __restrict__ meta)
 {
   const UnHeader h = un_header(f, n);
-  uint64_t nb = 0, st = h.st, r = h.r0;
+  uint64_t nb = 0, st = h.st, r = h.r0, maxLen = 0;
   // blocks until the end mark (smallz4cat.c:189-205, 345-349)
   while (st == 0) {
     if (r == n && h.legacy) break;
@@ -753,6 +753,7 @@ __device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, Un
     b.len = word;
     b.stored = packed ? 0u : 1u;
     blk[nb++] = b;
+    maxLen = word > maxLen ? word : maxLen;
     r += word;
     if (h.blockSum) {
       if (r + 4 > n) { st = 1; break; }
@@ -763,6 +764,7 @@ __device__ void unlz4_index_serial(const uint8_t* __restrict__ f, uint64_t n, Un
   meta[1] = st;
   meta[2] = h.legacy ? 1 : 0;
   meta[3] = 0;  // the serial walk decided
+  meta[4] = maxLen;
 }
 
 __global__ __launch_bounds__(64) void k_unlz4_index(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
@@ -979,7 +981,7 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
                                                         uint32_t* __restrict__ chain, UnBlock* __restrict__ blk,
                                                         uint64_t maxBlocks, uint64_t* __restrict__ meta)
 {
-  __shared__ uint32_t s_nb, s_st;
+  __shared__ uint32_t s_nb, s_st, s_max;
   __shared__ uint32_t s_link[kIxLds];  // the successors, when they fit: the walk then reads no HBM
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const UnHeader h = un_header(f, n);
@@ -988,6 +990,7 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
   const bool inLds = usable && M <= kIxLds;
   if (inLds)
     for (uint32_t i = tid; i < (uint32_t)M; i += 1024) s_link[i] = link[i];
+  if (tid == 0) s_max = 0;
   __syncthreads();
   if (tid < 64) {
     // one wavefront follows the successors from r0, 64 candidates per step: lane l holds candidate e + l
@@ -1050,6 +1053,7 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
     if (tid == 0) unlz4_index_serial(f, n, blk, maxBlocks, meta);
     return;
   }
+  uint32_t myMax = 0;
   for (uint32_t k = tid; k < nb; k += 1024) {
     const uint64_t r = list[chain[k]];
     uint32_t word = un_rd32(f, n, r);
@@ -1062,12 +1066,16 @@ __global__ __launch_bounds__(1024) void k_unlz4_ix_walk(const uint8_t* __restric
     b.len = word;
     b.stored = packed ? 0u : 1u;
     blk[k] = b;
+    myMax = word > myMax ? word : myMax;
   }
+  if (myMax) atomicMax(&s_max, myMax);
+  __syncthreads();
   if (tid == 0) {
     meta[0] = nb;
     meta[1] = st;
     meta[2] = h.legacy ? 1 : 0;
     meta[3] = 1;  // the parallel index decided
+    meta[4] = s_max;
   }
 }
 
