@@ -55,6 +55,12 @@
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
+#ifndef SZ4_LONG9_TAIL
+#define SZ4_LONG9_TAIL 1  // k_find_long9_hbm stages only the segment's targets in LDS (0: [w0, s1 + 64), A/B)
+#endif
+#ifndef SZ4_SCAN_DPP
+#define SZ4_SCAN_DPP 1  // 0: wavefront prefix scans by ds_bpermute instead of DPP row shifts + row broadcasts (A/B)
+#endif
 #ifndef SZ4_HBM_GLOBAL  // k_find_sorted_hbm reads the text from HBM/L2 (no LDS window): two workgroups per CU
 #define SZ4_HBM_GLOBAL 1
 #endif
@@ -246,6 +252,14 @@ __device__ __forceinline__ void wave_min4(uint32_t (&v)[4])
   }
 }
 
+// wave-wide max, result uniform
+__device__ __forceinline__ uint32_t wave_max_fast(uint32_t v)
+{
+  v = row_max(v);
+  const uint32_t a = rdlane(v, 0), b = rdlane(v, 16), c = rdlane(v, 32), d = rdlane(v, 48);
+  return max(max(a, b), max(c, d));
+}
+
 // wave-wide min, result uniform
 __device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
 {
@@ -254,8 +268,20 @@ __device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
   return min(min(a, b), min(c, d));
 }
 
+// inclusive wavefront scans by DPP: row shifts 1, 2, 4, 8, then lane 15 of each row into the next row and
+// lane 31 into rows 2-3, lanes without a source taking the identity (0 for + and unsigned max) -- six
+// dependent VALU steps instead of six ds_bpermute round trips
 __device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v)
 {
+#if SZ4_SCAN_DPP
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 1, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 2, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 4, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 8, 0xF, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast15, 0xA, 0xF, false);
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast31, 0xC, 0xF, false);
+  return v;
+#else
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -263,10 +289,20 @@ __device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v)
     if (lane >= (uint32_t)d) v += o;
   }
   return v;
+#endif
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v)
 {
+#if SZ4_SCAN_DPP
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 1, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 2, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 4, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 8, 0xF, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast15, 0xA, 0xF, false));
+  v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast31, 0xC, 0xF, false));
+  return v;
+#else
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -274,6 +310,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v)
     if (lane >= (uint32_t)d && o > v) v = o;
   }
   return v;
+#endif
 }
 
 // load that bypasses the vector L1 (sc1): for data this wavefront itself rewrote earlier in the
@@ -819,6 +856,18 @@ struct BytesHybrid {
   __device__ __forceinline__ uint32_t ld4(uint64_t pos) const
   {
     return pos + 8 <= lim ? lload4(w, (uint32_t)(pos - base)) : gload4(in, pos);
+  }
+};
+
+// [base, base + span) in LDS, every other byte from HBM/L2 (positions below base included)
+struct BytesTail {
+  const uint32_t* w;
+  uint64_t base, span;
+  const uint8_t* in;
+  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const
+  {
+    const uint64_t d = pos - base;  // wraps below base (so d + 8 could wrap too: compare d itself)
+    return d <= span - 8 ? lload4(w, (uint32_t)d) : gload4(in, pos);
   }
 };
 
@@ -1676,28 +1725,48 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       }
     } else {
     // 1. candidates inside the chunk, nearest first: a shift register -- after s shifts lane l holds
-      //    slot first + l - s -- walked while some lane's candidate is >= max(its group start, first)
+      //    slot first + l - s.  As at -9: a uniform trip count (the longest lane's) with a per-lane bound,
+      //    the lane's window start found by a binary search over the chunk (positions ascend with the lane
+      //    inside a group); a lane cut by its window has nothing left below the chunk.  Candidates stay in
+      //    order per lane, so the step count (strict improvements) is the reference's.
       {
         const int32_t lo1 = (int32_t)(gs > first ? gs : first);
-        uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
-        int32_t cl = (int32_t)slot;
-        bool walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
-        while (__ballot(walk)) {
+        uint32_t jLo = run && (int32_t)slot > lo1 ? (uint32_t)(lo1 - (int32_t)first) : lane;
+        bool cutHere = false;
+        if (needWin) {
+          uint32_t a = jLo, b = lane;  // the first lane j in [a, b) with myRel(j) >= lbRel, else b
+#pragma unroll
+          for (int it = 0; it < 6; it++) {
+            const uint32_t mid = (a + b) >> 1;
+            const uint32_t rj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(mid << 2), (int)myRel);
+            const bool go = a < b;
+            if (go && rj < lbRel) a = mid + 1u;
+            else if (go) b = mid;
+          }
+          cutHere = a > jLo;
+          jLo = a;
+        }
+        const uint32_t myCnt = lane - jLo;
+        const uint32_t rm = row_max(myCnt);
+        const uint32_t trips = max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
+        uint32_t r0 = me0, r1 = me1, r2 = me2;
+        auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kWaveShr1, 0xF, 0xF, true); };
+        for (uint32_t sft = 1; sft <= trips; sft++) {
 #if SZ4_DIAG == 3
           dL++;
 #endif
-          // (bound_ctrl: lane 0 receives 0 without an old value to set up)
-          rRel = (uint32_t)__builtin_amdgcn_mov_dpp((int)rRel, kWaveShr1, 0xF, 0xF, true);
-          r0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r0, kWaveShr1, 0xF, 0xF, true);
-          r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r1, kWaveShr1, 0xF, 0xF, true);
-          r2 = (uint32_t)__builtin_amdgcn_mov_dpp((int)r2, kWaveShr1, 0xF, 0xF, true);
-          cl--;
-          if (walk) {
-            if (needWin && rRel < lbRel) run = false;
-            if (run && test(r0, r1, r2) == 0u) improve(S.w0 + rRel, r1, r2);
+          r0 = shr1(r0);
+          r1 = shr1(r1);
+          r2 = shr1(r2);
+          const bool h = run && sft <= myCnt && test(r0, r1, r2) == 0u;
+          if (__ballot(h)) {
+            const uint32_t cRel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - sft) & 63u) << 2), (int)myRel);
+            if (h) improve(S.w0 + cRel, r1, r2);
           }
-          walk = walk && run && cl > lo1;
+          // lanes whose step count ran out stop early: leave when none is left with candidates
+          if ((sft & 7u) == 0u && !__ballot(run && sft < myCnt)) break;
         }
+        if (cutHere) run = false;
         // a lane whose group starts inside the chunk has seen all its candidates
         run = run && (int32_t)gs < (int32_t)first;
       }
@@ -2339,7 +2408,23 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     nEx = k;
     s_next = 0;
   }
-  // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM
+  // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM, or
+  // (SZ4_LONG9_TAIL) only the segment's own [s0, s1 + 64): 64 KiB, two workgroups per CU
+#if SZ4_LONG9_TAIL
+  typename std::conditional<kLds, Bytes<true>, BytesTail>::type src;
+  {
+    const uint64_t lo = kLds ? S.w0 : S.s0;
+    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
+    const uint32_t words = (uint32_t)((end - lo + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, lo + 4ull * i);
+    src.w = win;
+    src.base = lo;
+    if constexpr (!kLds) {
+      src.span = 4ull * words;
+      src.in = in;
+    }
+  }
+#else
   typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
   {
     const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
@@ -2352,6 +2437,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       src.in = in;
     }
   }
+#endif
   __syncthreads();
   const uint32_t ne = nEx;
   uint32_t E = (uint32_t)(S.s1 - S.w0);
@@ -2567,10 +2653,11 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
         got = prefix_if_at_least(src, p, c, need < 4u ? 4u : need, room);
         if (got < need) got = 0;
       }
-      // longest, then nearest (lower lane)
-      uint64_t top = wave_max_u64(got ? ((uint64_t)got << 6) | (63u - lane) : 0ull);
+      // longest, then nearest (lower lane); got <= room < 2^26, so the key fits 32 bits: a DPP row
+      // maximum and four readlanes instead of a 64-bit shuffle butterfly
+      const uint32_t top = wave_max_fast(got ? (got << 6) | (63u - lane) : 0u);
       if (top) {
-        const uint32_t tl = (uint32_t)(top >> 6), wl = 63u - (uint32_t)(top & 63u);
+        const uint32_t tl = top >> 6, wl = 63u - (top & 63u);
         const uint32_t wd = rdlane(dist, wl);
         if (tl > bestLen || (tl == bestLen && wd < bestDist)) {
           bestLen = tl;
@@ -2811,7 +2898,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(80))) 
 {
   find_long9_body<true>(SZ4_LONG9_PASS);
 }
-__global__ __launch_bounds__(kFindThreads) void k_find_long9_hbm(SZ4_LONG9_ARGS)
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(SZ4_LONG9_TAIL ? 80 : 102))) void k_find_long9_hbm(SZ4_LONG9_ARGS)
 {
   find_long9_body<false>(SZ4_LONG9_PASS);
 }
@@ -3845,8 +3932,21 @@ __device__ __forceinline__ uint32_t rmq_key(uint32_t cost, int32_t top, int32_t 
   return (cost << 8) | ((uint32_t)(top - j) & 255u);
 }
 
+// inclusive min-scan over the wavefront by DPP: row shifts 1, 2, 4, 8, then lane 15 of each row into the
+// next and lane 31 into rows 2-3 (lanes without a source take the identity) -- six dependent VALU steps
+// instead of six ds_bpermute round trips (the parse's range-minimum stores are latency-exposed)
 __device__ __forceinline__ uint32_t wave_incl_scan_min(uint32_t v)
 {
+#if SZ4_SCAN_DPP
+  constexpr int kId = (int)0xFFFFFFFFu;
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 1, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 2, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 4, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 8, 0xF, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowBcast15, 0xA, 0xF, false));
+  v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowBcast31, 0xC, 0xF, false));
+  return v;
+#else
   const uint32_t lane = lane_id();
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -3854,6 +3954,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan_min(uint32_t v)
     if (lane >= (uint32_t)d && o < v) v = o;
   }
   return v;
+#endif
 }
 
 // UP of the chunk [hi - cnt + 1, hi] (lane t = position hi - t, key kt).  The chunk lies inside one
@@ -5466,8 +5567,8 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         chain.valid = chain.pending = false;
         if (!noMatch) {  // convergence bookkeeping (a segment without matches never converges)
           const uint32_t delta = cT - cC;
-          uint32_t dPrev = __shfl_up(delta, 1, 64);
-          if (lane == 0) dPrev = prevDelta;
+          // the previous position's delta: wave_shr:1, lane 0 takes the carried one (the DPP's old value)
+          const uint32_t dPrev = (uint32_t)__builtin_amdgcn_update_dpp((int)prevDelta, (int)delta, kWaveShr1, 0xF, 0xF, false);
           const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
           if (chg) runTop = h - (63 - (int32_t)__builtin_clzll(chg));
           prevDelta = rdlane(delta, cnt - 1u);
@@ -5508,8 +5609,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
         if (closedE > maxReach) maxReach = closedE;
         if (closedE != chain.E) chain.valid = chain.pending = false;
         const uint32_t delta = cT - cC;
-        uint32_t dPrev = __shfl_up(delta, 1, 64);
-        if (lane == 0) dPrev = prevDelta;
+        const uint32_t dPrev = (uint32_t)__builtin_amdgcn_update_dpp((int)prevDelta, (int)delta, kWaveShr1, 0xF, 0xF, false);
         const uint64_t chg = __ballot(lane < cnt && (ip == hi || delta != dPrev));
         const uint64_t upTo = lane == 63u ? ~0ull : ((2ull << lane) - 1ull);
         const int32_t rt = (chg & upTo) ? h - (63 - (int32_t)__builtin_clzll(chg & upTo)) : runTop;
@@ -6398,9 +6498,11 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
         for (uint32_t resolve = 0; resolve < 2; resolve++)
           hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
                              compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
-      hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+      // (SZ4_LONG9_TAIL: the segment's own 64 Ki targets and 64 bytes more)
+      const uint32_t l9Lds = SZ4_LONG9_TAIL ? 65536u + 256u : hybridLds;
+      hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l9Lds);
       for (int fix = 0; fix < 2; fix++)
-        hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+        hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), l9Lds, s, in, segs, blocks, iv, ivCount,
                            compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen, specDist,
                            fix);
     }
