@@ -79,13 +79,17 @@ __device__ __forceinline__ uint32_t un_wrlane(uint32_t v, uint32_t x, uint32_t l
   return (uint32_t)sz4_un_writelane((int)x, (int)l, (int)v);
 }
 
+// inclusive add-scan over the 64 lanes by DPP (row shifts 1, 2, 4, 8, then the row broadcasts): six
+// dependent VALU steps instead of six ds_bpermute round trips
 __device__ __forceinline__ uint32_t un_incl_scan_add(uint32_t v, uint32_t lane)
 {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += o;
-  }
+  (void)lane;
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
   return v;
 }
 
