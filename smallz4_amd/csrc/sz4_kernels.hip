@@ -55,6 +55,9 @@
 #ifndef SZ4_LEAN_SHIFT
 #define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
 #endif
+#ifndef SZ4_BIG_OCC
+#define SZ4_BIG_OCC 1  // k_find_big at 8 waves per SIMD (64 VGPRs; above 64 KiB blocks only the targets in LDS)
+#endif
 #ifndef SZ4_LONG9_TAIL
 #define SZ4_LONG9_TAIL 1  // k_find_long9_hbm stages only the segment's targets in LDS (0: [w0, s1 + 64), A/B)
 #endif
@@ -2972,7 +2975,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   } while (0)
 #endif
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ4_BIG_OCC ? 8 : 1), amdgpu_num_sgpr(SZ4_BIG_OCC ? 80 : 102))) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                            const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                            const uint32_t* __restrict__ ivCount,
                                                            const uint2* __restrict__ compactAll, uint2* __restrict__ scratchAll,
@@ -3110,6 +3113,23 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
   // the second launch only resolves: a segment's first big targets need its predecessor segment's
   // last results, final after the first launch
   if (!resolveOnly) {
+#if SZ4_BIG_OCC
+  // two workgroups per CU (<= 64 VGPRs): blocks above 64 KiB stage only the segment's own targets
+  // [s0, s1 + 64) in LDS, the 64 KiB below them come from HBM/L2
+  typename std::conditional<kLds, Bytes<true>, BytesTail>::type src;
+  {
+    const uint64_t lo = kLds ? S.w0 : S.s0;
+    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
+    const uint32_t words = (uint32_t)((end - lo + 3) / 4);
+    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, lo + 4ull * i);
+    src.w = win;
+    src.base = lo;
+    if constexpr (!kLds) {
+      src.span = 4ull * words;
+      src.in = in;
+    }
+  }
+#else
   typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
   {
     const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
@@ -3122,6 +3142,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find_big(const uint8_t* __rest
       src.in = in;
     }
   }
+#endif
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone when that is not a chain position
   // (then the position is always left-maximal)
@@ -4833,8 +4854,9 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
       nxt = q + 64 <= segHi ? L[q + 64] : 0u;
       const uint32_t v = q <= segHi ? (uint32_t)q + Lq : 0u;
       const uint32_t incl = wave_incl_scan_max(v);
-      uint32_t excl = __shfl_up(incl, 1, 64);
-      excl = lane == 0 ? carry : (excl > carry ? excl : carry);
+      // exclusive: wave_shr:1 by DPP, lane 0 takes the carry (the DPP's old value)
+      uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp((int)carry, (int)incl, kWaveShr1, 0xF, 0xF, false);
+      excl = excl > carry ? excl : carry;
       if (q <= segHi) R[q] = excl;
       const uint32_t top = rdlane(incl, 63);
       carry = top > carry ? top : carry;
@@ -6493,10 +6515,12 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                          compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
     }
     else if (unlimited) {
-      hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hybridLds);
+      // (SZ4_BIG_OCC: the segment's own 64 Ki targets and 64 bytes more)
+      const uint32_t bigLds = SZ4_BIG_OCC ? 65536u + 256u : hybridLds;
+      hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bigLds);
       if (!getenv("SZ4_NO_BIG"))
         for (uint32_t resolve = 0; resolve < 2; resolve++)
-          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), hybridLds, s, in, segs, blocks, iv, ivCount,
+          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), bigLds, s, in, segs, blocks, iv, ivCount,
                              compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
       // (SZ4_LONG9_TAIL: the segment's own 64 Ki targets and 64 bytes more)
       const uint32_t l9Lds = SZ4_LONG9_TAIL ? 65536u + 256u : hybridLds;
