@@ -65,7 +65,7 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
  * Any n in bounded memory: the blocks are compressed in pieces of at most
- * sz4_set_batch_chunk bytes (1 GiB by default: about 36-60 GB of scratch; under a
+ * sz4_set_batch_chunk bytes (1.5 GiB by default: about 54-90 GB of scratch; under a
  * sz4_set_device_limit bound the pieces shrink to about 1/64 of it).
  *
  *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
@@ -121,7 +121,7 @@ int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_by
 void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
- * device scratch is about 36-60 bytes per piece byte.  0 restores the 1 GiB default. */
+ * device scratch is about 36-60 bytes per piece byte.  0 restores the 1.5 GiB default. */
 void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured

@@ -32,9 +32,11 @@ namespace {
 
 constexpr uint64_t kPad = 64;                 // bytes of slack after every staged input
 constexpr uint64_t kSegTargets = 65536;       // target positions per segment
-// batch API pieces: 1 GiB of input (36-60 GB of scratch, sized for the MI355X's 288 GB): at 256 KiB
-// blocks a piece is 4096 blocks, four of the per-block repair wavefronts per SIMD instead of one
-constexpr uint64_t kBatchChunkDefault = 1ull << 30;
+// batch API pieces: 1.5 GiB of input (54-90 GB of scratch, sized for the MI355X's 288 GB): a rank's
+// 1.25 GiB slice of configs[4] is ONE piece (the per-block repair wavefronts of its 5120 blocks run
+// together: one latency-bound walk instead of one per piece), and a piece of 256 KiB blocks holds four
+// or more repair wavefronts per SIMD
+constexpr uint64_t kBatchChunkDefault = 3ull << 29;
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
 // dictionary rounds before the in-order replay takes the chunk: each round settles at least one more
 // shortcut interval of every block, so a chunk needs at most (intervals per block) + 1 rounds, and a block
