@@ -371,7 +371,8 @@ __global__ __launch_bounds__(256) void k_dict_pe(const uint8_t* __restrict__ in,
 // findLongestMatch (smallz4.h:173-255) of every linked position (previousExact set) of every block,
 // over snapshot reads of the exact chains: strictly longer replaces, maxChain counts replacements.
 // Every other position gets (0, 0): not searched.  Grid (positions, blocks).
-__global__ __launch_bounds__(256) void k_dict_search(const uint8_t* __restrict__ in, DictPlan P, uint32_t maxChain,
+// (8 waves per SIMD: the chain walks are latency-bound; 65 VGPRs / 100 SGPRs admitted 6)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_num_sgpr(80))) void k_dict_search(const uint8_t* __restrict__ in, DictPlan P, uint32_t maxChain,
                                                      const uint16_t* __restrict__ pe, const uint16_t* __restrict__ prevX0,
                                                      uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
                                                      uint32_t* __restrict__ sel, uint32_t* __restrict__ longFlag)
