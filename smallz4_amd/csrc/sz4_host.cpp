@@ -609,7 +609,9 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
     if ((e = hipMemsetAsync(c->status.p, 0, 4, s)) || (e = hipMemsetAsync(c->longFlag.p, 0, nb * 4, s)))
       return c->fail(SZ4_E_DEVICE, "prep", e);
   }
-  launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), dIvN, maxChain, c->mlen.as<uint32_t>(),
+  uint32_t maxDpCount = 1;
+  for (const Block& B : c->hBlocks) maxDpCount = std::max(maxDpCount, B.dpCount);
+  launch_parse(in, dB, nb, c->dpSegs.as<DpSeg>(), (uint32_t)c->hDp.size(), maxDpCount, dIvN, maxChain, c->mlen.as<uint32_t>(),
                c->mdist.as<uint16_t>(), 0, c->cost.as<uint32_t>(), c->sel(), c->reach.as<uint32_t>(),
                c->segState.as<uint4>(), c->longFlag.as<uint32_t>(), c->rmqUp(), c->rmqDown(),
                c->dpSide(), c->dpRec.as<uint4>(),

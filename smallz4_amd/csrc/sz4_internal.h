@@ -173,8 +173,9 @@ void launch_lazy(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
                  Interval* iv, uint32_t* ivCount, const uint32_t* longFlag, uint32_t* mlen, const uint16_t* mdist,
                  uint64_t matchBase, uint32_t* slots, uint4* state, uint32_t* firstBad, int* status, hipStream_t s);
 uint32_t lazy_slots_per_walk();
+// maxDpCount: the largest dpCount of the launch's blocks (sizes k_dp_fix<false>'s LDS tables)
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
-                  const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
+                  uint32_t maxDpCount, const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist,
                   uint64_t matchBase, uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState,
                   const uint32_t* longFlag, uint32_t* rmqUp, uint32_t* rmqDown, uint2* dpSide, uint4* dpRec, int* status,
                   hipStream_t s);

@@ -5332,14 +5332,16 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
                                                uint32_t* __restrict__ sel, const uint32_t* __restrict__ reach,
                                                uint4* __restrict__ segState, const uint32_t* __restrict__ longFlag,
                                                uint32_t* __restrict__ upAll, uint32_t* __restrict__ downAll,
-                                               uint2* __restrict__ side, uint4* __restrict__ dpRec)
+                                               uint2* __restrict__ side, uint4* __restrict__ dpRec, uint32_t tabStride)
 {
   __shared__ uint32_t ring[kRing];
-  constexpr uint32_t kTab = kPar ? 1u : kMaxDpSegs;
-  __shared__ uint32_t convTab[kTab];   // positions >= convTab[k] of segment k: exact = stored + aboveTab[k]
-  __shared__ uint32_t deltaTab[kTab];  // below it: exact = stored + deltaTab[k]
-  __shared__ uint32_t convBlk[kTab];   // UP/DOWN keys of positions below it: exact = key cost + deltaTab[k]
-  __shared__ uint32_t aboveTab[kTab];  // 0, or the offset of the segment above when k_dp_fix<true> repaired it
+  // k_dp_fix<false>: four tables of tabStride (the launch's largest dpCount) words in dynamic LDS -- sized
+  // for kMaxDpSegs they held 32 KiB and let only four of these one-wave workgroups share a CU
+  extern __shared__ __attribute__((aligned(16))) uint32_t dpTab[];
+  uint32_t* const convTab = dpTab;                   // positions >= convTab[k] of segment k: exact = stored + aboveTab[k]
+  uint32_t* const deltaTab = dpTab + tabStride;      // below it: exact = stored + deltaTab[k]
+  uint32_t* const convBlk = dpTab + 2 * tabStride;   // UP/DOWN keys of positions below it: exact = key cost + deltaTab[k]
+  uint32_t* const aboveTab = dpTab + 3 * tabStride;  // 0, or the offset of the segment above when k_dp_fix<true> repaired it
   uint32_t bIdx, kFirst, kEnd;
   if constexpr (kPar) {
     if (blockIdx.x >= ndp) return;
@@ -5771,7 +5773,7 @@ __global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks,
           };
           rmq_store_up_block(up, top, jb, jt, exact);
           rmq_store_down(down, top, jb, exact);
-          if (lane == 0) convBlk[k] = (uint32_t)jb;
+          if (!kPar && lane == 0) convBlk[k] = (uint32_t)jb;  // (k_dp_fix<true> has no tables)
         }
       }
     }
@@ -6565,7 +6567,7 @@ void launch_lazy(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
 uint32_t lazy_slots_per_walk() { return 2 * kLazyCap; }
 
 void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, const DpSeg* dpSegs, uint32_t ndp,
-                  const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
+                  uint32_t maxDpCount, const uint32_t* ivCount, uint32_t maxChain, uint32_t* mlen, const uint16_t* mdist, uint64_t matchBase,
                   uint32_t* cost, uint32_t* sel, uint32_t* reach, uint4* segState, const uint32_t* longFlag, uint32_t* rmqUp,
                   uint32_t* rmqDown, uint2* dpSide, uint4* dpRec, int* status, hipStream_t s)
 {
@@ -6578,9 +6580,10 @@ void launch_parse(const uint8_t* in, const Block* blocks, uint32_t nblocks, cons
   hipLaunchKernelGGL(k_dp_spec_rmq, dim3((ndp + kSpecWaves - 1) / kSpecWaves), dim3(64 * kSpecWaves), 0, s, blocks, dpSegs,
                      ndp, mlen, mdist, matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown);
   hipLaunchKernelGGL(k_dp_fix<true>, dim3(ndp), dim3(64), 0, s, blocks, dpSegs, ndp, mlen, mdist, matchBase, cost, sel,
-                     reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec);
-  hipLaunchKernelGGL(k_dp_fix<false>, dim3(nblocks), dim3(64), 0, s, blocks, dpSegs, ndp, mlen, mdist, matchBase, cost, sel,
-                     reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec);
+                     reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec, 0u);
+  const uint32_t tab = maxDpCount < 1u ? 1u : maxDpCount > kMaxDpSegs ? kMaxDpSegs : maxDpCount;
+  hipLaunchKernelGGL(k_dp_fix<false>, dim3(nblocks), dim3(64), 4 * tab * sizeof(uint32_t), s, blocks, dpSegs, ndp, mlen, mdist,
+                     matchBase, cost, sel, reach, segState, longFlag, rmqUp, rmqDown, dpSide, dpRec, tab);
 }
 
 void launch_emit(const uint8_t* in, const Block* blocks, uint32_t nblocks, const uint2* walkSegs, uint32_t nwalk,
