@@ -5295,7 +5295,14 @@ __global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4
 {
   dp_spec_body<false>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
+#ifndef SZ4_RMQ_SGPR
+#define SZ4_RMQ_SGPR 0  // k_dp_spec_rmq's SGPR budget (0: the compiler's)
+#endif
+#if SZ4_RMQ_SGPR
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4_RMQ_SGPR))) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
+#else
 __global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
+#endif
 {
   dp_spec_body<true>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
