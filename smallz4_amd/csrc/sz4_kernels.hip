@@ -5296,7 +5296,7 @@ __global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4
   dp_spec_body<false>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
 #ifndef SZ4_RMQ_SGPR
-#define SZ4_RMQ_SGPR 0  // k_dp_spec_rmq's SGPR budget (0: the compiler's)
+#define SZ4_RMQ_SGPR 80  // k_dp_spec_rmq's SGPR budget (80: 8 waves per SIMD; 0: the compiler's, 106 -> 7 waves)
 #endif
 #if SZ4_RMQ_SGPR
 __global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4_RMQ_SGPR))) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
@@ -5331,8 +5331,16 @@ constexpr uint32_t kDpSideStride = kDpSide + kDpSideKeys;
 #endif
 constexpr uint32_t kParRmqMinSegs = SZ4_PAR_RMQ_MIN;
 
+#ifndef SZ4_FIX_SGPR
+#define SZ4_FIX_SGPR 0  // k_dp_fix's SGPR budget (0: the compiler's)
+#endif
 template <bool kPar>
-__global__ __launch_bounds__(64) void k_dp_fix(const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
+#if SZ4_FIX_SGPR
+__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(SZ4_FIX_SGPR))) void k_dp_fix(
+#else
+__global__ __launch_bounds__(64) void k_dp_fix(
+#endif
+const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
                                                uint32_t ndp, const uint32_t* __restrict__ mlen,
                                                const uint16_t* __restrict__ mdist,
                                                uint64_t matchBase, uint32_t* __restrict__ costAll,
