@@ -144,6 +144,8 @@ def parse_args(argv=None):
     ap.add_argument("--level-cpu-seconds", type=float, default=3.0, help="levels leg: budget of each CPU baseline sample")
     ap.add_argument("--shape-steps", type=int, default=3)
     ap.add_argument("--shape-verify-seconds", type=float, default=8.0)
+    ap.add_argument("--silesia-verify-seconds", type=float, default=150.0,
+                    help="configs[2]'s diff budget: enough for all 51 blocks (the reference takes 10-60 s per 4 MiB block)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: gloo ranks compress their shards with the oracle (tests the sharding)")
     a = ap.parse_args(argv)
@@ -324,6 +326,22 @@ def valu_ceiling():
         return None
     out.update({"vgpr": round(best / 1024 / (CLOCK_GHZ * 1e9), 4), "clock_ghz": CLOCK_GHZ, "variant": "add_xor"})
     return out
+
+
+def summary_line(rec) -> str:
+    """A short plain-text recap printed after the JSON line (not JSON, so nothing parses it as the
+    record): the headline's own parity and roofline, and each shape's rate and diff, where a log tail
+    that cuts the long line still shows them."""
+    ver = rec.get("verify", {})
+    parts = [f"summary: value {rec['value']} MB/s", f"byte_diff {rec['byte_diff']}",
+             f"blocks_verified {rec['blocks_verified']}/{ver.get('blocks_total', '?')}",
+             f"roundtrip_ok {rec['roundtrip_ok']}", f"roofline.frac {rec['roofline']['frac']}"]
+    for label, sh in (rec.get("shapes") or {}).items():
+        parts.append(f"{label} {sh['MB/s']} MB/s byte_diff {sh.get('byte_diff')} "
+                     f"({sh.get('blocks_verified')}/{sh.get('blocks_total')} blocks, verify_complete {sh.get('verify_complete')})")
+    for lv, r in ((rec.get("levels") or {}).get("levels") or {}).items():
+        parts.append(f"level {lv} {r['MB/s']} MB/s byte_diff {r.get('byte_diff')}")
+    return "; ".join(parts)
 
 
 def spawn_ranks(args):
@@ -575,7 +593,10 @@ def shapes_leg(args, run: Runner, chain: int, enwik8_data: bytes):
                "stages_ms": {k: round(v, 3) for k, v in stages.items()}, "generate_s": round(gen_s, 1),
                "unlz4": rt}
         if not args.no_verify:
-            rec.update(verify_sample(part, data, bs, chain, args.verify_threads, args.shape_verify_seconds, every=False))
+            # configs[2] is diffed in full (every block, `every`), the others on a sample cut at the budget
+            full = label == "silesia_4m"
+            budget = args.silesia_verify_seconds if full else args.shape_verify_seconds
+            rec.update(verify_sample(part, data, bs, chain, args.verify_threads, budget, every=full))
         res[label] = rec
         print(json.dumps({"shape": label, **rec}), file=sys.stderr, flush=True)
         del data, part
@@ -757,6 +778,7 @@ def main():
         # the reference on this host's cores, rank 0, after the timed region (at every N)
         rec["cpu_baseline"] = cpu_baseline(data, bs, chain, args.cpu_seconds)
         print(json.dumps(rec), flush=True)
+        print(summary_line(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

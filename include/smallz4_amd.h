@@ -203,8 +203,9 @@ void sz4_set_pool_cap(uint64_t bytes);
  * SZ4_DICT_MAX_ROUNDS in the environment when the context was created). */
 uint32_t sz4_dict_rounds(sz4_ctx* ctx);
 
-/* Decoder diagnostics: the pointer-jumping passes (k_unlz4_resolve, one host round trip each) the last
- * decode took in split mode (frames with blocks of >= 256 KiB payload), 0 when it decoded block by block. */
+/* Decoder diagnostics: the longest reference chain (hops to earlier sub-segments) the last split-mode decode
+ * followed while packing its output (frames with blocks of >= 256 KiB payload), 0 when it decoded block by
+ * block or no byte referred to another sub-segment. */
 uint32_t sz4_unlz4_resolve_passes(sz4_ctx* ctx);
 /* 1 when the last decode's block index came from the parallel index, 0 when the serial size-word walk
  * decided (a malformed frame, too many candidates, or SZ4_UNLZ4_INDEX=0). */

@@ -49,9 +49,6 @@ namespace sz4 {
 constexpr uint32_t kDictNoPos = 0xFFFFFFFFu;
 constexpr uint32_t kDictPosBits = 23;  // a block's insertions and the 64 KiB below them: < 2^23 positions
 constexpr uint64_t kDictPosMask = (1ull << kDictPosBits) - 1;
-#ifndef SZ4_DICT_RUNSKIP
-#define SZ4_DICT_RUNSKIP 1  // k_dict_search steps over a run's 1-hop chain stretches (0: A/B)
-#endif
 constexpr uint32_t kDictSkipKey = 1u << kHashBits;  // k_dict_keys: a shortcut position (sorts after every hash)
 constexpr uint32_t kDictSortBits = kHashBits + 1 + kDictPosBits;
 
@@ -407,7 +404,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
       const int64_t need = (int64_t)bestLen + 1;
       if (need > room) break;
       uint64_t c = pos - backDist;
-#if SZ4_DICT_RUNSKIP
       if (hop == 1u && bestLen >= 4u) {
         // In a run of one byte value v every inserted position's exact predecessor is the one before it,
         // so the chain steps down the run one position at a time.  Once p holds a match of bestLen and
@@ -434,7 +430,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
           }
         }
       }
-#endif
       // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
       int64_t lo = need - 4;
       while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;

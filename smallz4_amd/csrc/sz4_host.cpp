@@ -37,6 +37,8 @@ constexpr uint64_t kSegTargets = 65536;       // target positions per segment
 // together: one latency-bound walk instead of one per piece), and a piece of 256 KiB blocks holds four
 // or more repair wavefronts per SIMD
 constexpr uint64_t kBatchChunkDefault = 3ull << 29;
+constexpr uint64_t kScratchPerByte = 50;     // device scratch per piece byte, upper bound (36-49 measured)
+constexpr uint64_t kPieceFloor = 16ull << 20;  // smallest batch piece the out-of-memory retry goes down to
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
 // dictionary rounds before the in-order replay takes the chunk: each round settles at least one more
 // shortcut interval of every block, so a chunk needs at most (intervals per block) + 1 rounds, and a block
@@ -97,6 +99,11 @@ struct DevBuf {
     if (bud) bud->used -= cap;
     p = nullptr;
     cap = 0;
+  }
+  // the context could grow this buffer to `bytes` without releasing any other buffer
+  bool fits(size_t bytes) const
+  {
+    return bytes <= cap || !bud || !bud->limit || bud->used - cap + bytes <= bud->limit;
   }
   template <class T>
   T* as() const { return static_cast<T*>(p); }
@@ -181,7 +188,6 @@ struct sz4_ctx {
   uint32_t lastBlocks = 0;
   int stopAfter = 0;
   uint32_t lastChain = 0;
-  bool separateSort = false;  // k_sort runs inside k_find_sorted; SZ4_SEPARATE_SORT=1: its own launch
 
   DevBuf staged, blocks, segs, iv, ivCount, rank, mlen, mdist, cost, ntok, blockBytes, offsets, status;
   DevBuf dpSegs, reach, segState, walkSegs, walkState, longFlag, longBits, segLong, segTail;
@@ -214,6 +220,7 @@ struct sz4_ctx {
   HostBuf hostIn[2], hostOut[2];
   uint64_t streamChunk = 64ull << 20;  // stream path: input bytes per chunk (rounded to whole blocks)
   uint64_t batchChunk = kBatchChunkDefault;  // sz4_compress_blocks_device: input bytes per internal pipeline run
+  bool batchChunkSet = false;          // set explicitly (sz4_set_batch_chunk, SZ4_BATCH_CHUNK): no free-memory cap
   bool batchChunked = false;           // the last sz4_compress_blocks_device call ran in several pieces
   uint64_t streamPlanKey[5] = {~0ull, 0, 0, 0, 0};  // stream path: the chunk shape the current plan is for
   // stream path, chunk continuation: the previous chunk's last block's final shortcut intervals
@@ -229,7 +236,7 @@ struct sz4_ctx {
   std::vector<UnBlock> hUn;
   std::vector<UnSub> hSub;
   bool unSplit = false;  // the last planned frame decodes in split mode
-  uint32_t unResolvePasses = 0;  // pointer-jumping passes the last split-mode decode took
+  uint32_t unResolvePasses = 0;  // the longest reference chain the last split-mode decode's pack followed
   bool unIndexParallel = false;  // the last frame index came from the parallel index (not the serial walk)
   int unSplitMode = getenv("SZ4_UNLZ4_SPLIT") ? atoi(getenv("SZ4_UNLZ4_SPLIT")) : -1;  // -1 auto, 0 never, 1 always
   int64_t dictBack = -1;       // >= 0: dictionary mode, first insertion this far before the first block
@@ -246,7 +253,6 @@ struct sz4_ctx {
   // plan: repeated calls on the same shape skip the uploads
   uint64_t planVersion = 0, uploadedVersion = ~0ull;
   const void* uploadedAt[4] = {};
-  uint32_t hybridLds = 0;  // k_find_long9's LDS staging when the window is not LDS-resident
   // plan cache for sz4_compress_blocks_device
   uint64_t planN = ~0ull;
   uint32_t planBS = 0;
@@ -354,15 +360,11 @@ void finish_plan(sz4_ctx* c)
       if (lo == 0) break;
     }
   }
-  // SZ4_FIND_HBM=1 (A/B only): the finders read the text from HBM/L2 even when the window fits LDS
-  static const bool forceHbm = getenv("SZ4_FIND_HBM") != nullptr;
-  c->ldsWindow = !forceHbm;
-  c->hybridLds = 0;
+  // the finders' LDS-window kernels take the launch when every block's window fits their LDS
+  c->ldsWindow = true;
   for (const Segment& S : c->hSegs) {
     const Block& B = c->hBlocks[S.block];
     if ((B.end - S.w0 + 8 + 3) / 4 * 4 > find_lds_bytes()) c->ldsWindow = false;
-    const uint64_t end = std::min<uint64_t>(S.s1 + 64, B.end + 8);
-    c->hybridLds = std::max<uint32_t>(c->hybridLds, (uint32_t)((end - S.w0 + 3) / 4 * 4));
   }
 }
 
@@ -574,22 +576,19 @@ int run_pipeline(sz4_ctx* c, uint32_t maxChain, const uint8_t* in, const uint8_t
       // marker bits are OR-ed in
       if ((e = hipMemsetAsync(c->longBits.p, 0, c->hBlocks.back().end / 8 + 8, s)))
         return c->fail(SZ4_E_DEVICE, "clear matches", e);
-      // k_find_sorted sorts its own segment first unless SZ4_SEPARATE_SORT=1
-      if (c->separateSort)
-        launch_sort(in, dS, ns, dB, dIv, dIvN, c->elemA(), c->elemB(), c->rank.as<uint32_t>(), s);
     }
     mark(c, 2, s);
     if (maxChain > 0)
       launch_find(1, in, dS, ns, dB, dIv, dIvN, c->elemB(), c->elemA(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
-                  nullptr, nullptr, nullptr, nullptr, c->ldsWindow, c->hybridLds, !c->separateSort, s);
+                  nullptr, nullptr, nullptr, nullptr, c->ldsWindow, s);
     mark(c, 3, s);
     if (c->stopAfter == 2) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     if (maxChain > 0)
       launch_find(2, in, dS, ns, dB, dIv, dIvN, c->elemB(), c->elemA(), c->rank.as<uint32_t>(), maxChain,
                   c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->longBits.as<uint32_t>(), c->segLong.as<uint32_t>(),
                   c->longFlag.as<uint32_t>(), c->cost.as<uint32_t>(), c->reach.as<uint32_t>(), c->segTail.as<uint64_t>(),
-                  c->ldsWindow, c->hybridLds, false, s);
+                  c->ldsWindow, s);
     mark(c, 4, s);
     if (c->stopAfter == 3) return hipStreamSynchronize(s) == hipSuccess ? SZ4_OK : c->fail(SZ4_E_DEVICE, "pipeline");
     launch_prep(in, dB, nb, dIv, dIvN, maxChain, c->mlen.as<uint32_t>(), c->mdist.as<uint16_t>(), 0, c->sel(),
@@ -668,13 +667,18 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   for (;;) {
     if ((e = c->unBlk.reserve(maxBlocks * sizeof(UnBlock) + 64)) || (e = c->unMeta.reserve(64)))
       return c->fail(SZ4_E_NOMEM, "decoder scratch", e);
-    // the parallel index (its scratch is about 3n / 8 bytes); the one-lane walk when that does not fit
-    if (!c->unIndexSerial && c->unIx.reserve(unlz4_ix_scratch_bytes(n)) == hipSuccess)
+    // the parallel index (its scratch is about 3n / 8 bytes); the one-lane walk when that does not fit.  Under a
+    // device bound it is tried only if it fits without releasing other buffers (it is optional: ADVICE r05)
+    const uint64_t ixBytes = unlz4_ix_scratch_bytes(n);
+    if (!c->unIndexSerial && c->unIx.fits(ixBytes) && c->unIx.reserve(ixBytes) == hipSuccess)
       launch_unlz4_index_par(f, n, c->unIx.p, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
     else
       launch_unlz4_index(f, n, c->unBlk.as<UnBlock>(), maxBlocks, c->unMeta.as<uint64_t>(), s);
     if ((e = hipMemcpyAsync(meta, c->unMeta.p, sizeof meta, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
       return c->fail(SZ4_E_DEVICE, "frame index", e);
+    // the index scratch is dead once its result is read: kept for the next call, but releasable by a
+    // growing reservation of this one (the split buffers, the output)
+    c->unIx.lastGen = 0;
     if (meta[1] != 2) break;
     maxBlocks = n / 5 + 2;
   }
@@ -707,12 +711,12 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
       UnBlock& B = c->hUn[b];
       B.subFirst = (uint32_t)c->hSub.size();
       B.subCount = (B.len + kUnSub - 1) / kUnSub;
-      for (uint32_t k = 0; k < B.subCount; k++) c->hSub.push_back(UnSub{b, k, 0, 0, 0, 0, 0, 0, 0, 0});
+      for (uint32_t k = 0; k < B.subCount; k++) c->hSub.push_back(UnSub{b, k});
     }
     const uint32_t nsub = (uint32_t)c->hSub.size();
     if ((e = c->unSeq.reserve((uint64_t)nsub * 2 * kUnSubCap * sizeof(uint4) + 64)) ||
         (e = c->unSubs.reserve((uint64_t)nsub * sizeof(UnSub) + 64)) ||
-        (e = c->unMasks.reserve((uint64_t)nsub * (kUnSub / 8) + 64))) {
+        (e = c->unMasks.reserve((uint64_t)nsub * kUnAuxWords * 4 + 64))) {
       c->unSeq.release();
       return blockwise();
     }
@@ -760,6 +764,26 @@ int unlz4_plan(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32
   return SZ4_OK;
 }
 
+// the device output buffer of the host-buffer decoders (sz4_unlz4, the stream decoder): when it does not fit
+// beside a split-mode plan, the frame is planned again block by block (about half the scratch) and the
+// reservation retried (the split plan's own check did not count this buffer)
+int unlz4_reserve_out(sz4_ctx* c, const uint8_t* f, uint64_t n, uint64_t* total, uint32_t* keep)
+{
+  hipError_t e = c->unOut.reserve(*total);
+  if (e == hipSuccess) return SZ4_OK;
+  if (c->unSplit) {
+    for (DevBuf* b : {&c->unSubs, &c->unMasks, &c->unImage, &c->unSeq, &c->unIx}) b->release();
+    const int mode = c->unSplitMode;
+    c->unSplitMode = 0;
+    const int r = unlz4_plan(c, f, n, total, keep, nullptr);
+    c->unSplitMode = mode;
+    if (r) return r;
+    e = c->unOut.reserve(*total);
+    if (e == hipSuccess) return SZ4_OK;
+  }
+  return c->fail(SZ4_E_NOMEM, "output", e);
+}
+
 int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, uint64_t dl, uint8_t* out, uint32_t keep,
                  hipStream_t s)
 {
@@ -776,20 +800,15 @@ int unlz4_decode(sz4_ctx* c, const uint8_t* f, uint64_t n, const uint8_t* dict, 
       return c->fail(SZ4_E_DEVICE, "decoder plan", e);
     launch_unlz4_split_decode(f, n, c->unBlk.as<UnBlock>(), c->unSubs.as<UnSub>(), nsub, c->unSeq.as<uint4>(),
                               c->unImage.as<uint32_t>(), dict, dl, s);
-    // every pass at least halves the longest reference chain (a chain steps to an earlier sub-segment)
-    c->unResolvePasses = 0;
-    for (int pass = 0;; pass++) {
-      c->unResolvePasses = (uint32_t)pass + 1;
-      uint32_t left = 0;
-      if ((e = hipMemsetAsync(flag, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
-      launch_unlz4_resolve(c->unImage.as<uint32_t>(), total, flag, s);
-      if ((e = hipMemcpyAsync(&left, flag, 4, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
-        return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
-      if (!left) break;
-      if (pass > 64) return c->fail(SZ4_E_DEVICE, "decoder references did not resolve");
-    }
-    launch_unlz4_pack(c->unImage.as<uint32_t>(), total, out, s);
-    if ((e = hipGetLastError()) || (e = hipStreamSynchronize(s))) return c->fail(SZ4_E_DEVICE, "decode", e);
+    // the pack follows every reference chain to its byte (each hop lands in an earlier sub-segment): no
+    // host round trip between passes; unResolvePasses reports the longest chain
+    if ((e = hipMemsetAsync(flag, 0, 4, s))) return c->fail(SZ4_E_DEVICE, "decoder resolve", e);
+    launch_unlz4_pack(c->unImage.as<uint32_t>(), total, out, flag, s);
+    uint32_t hops = 0;
+    if ((e = hipGetLastError()) || (e = hipMemcpyAsync(&hops, flag, 4, hipMemcpyDeviceToHost, s)) ||
+        (e = hipStreamSynchronize(s)))
+      return c->fail(SZ4_E_DEVICE, "decode", e);
+    c->unResolvePasses = hops;
     return SZ4_OK;
   }
   const uint64_t flagBytes = ((uint64_t)keep + 2) * 4;
@@ -1216,7 +1235,7 @@ int stream_decompress(sz4_ctx* c, sz4_get_byte get, sz4_send_out send, const uin
     if (int r = unlz4_plan(c, c->unFrame.as<uint8_t>(), fl, &size, &keep, nullptr)) return r;
     out.resize(size);
     if (size) {
-      if ((e = c->unOut.reserve(size))) return c->fail(SZ4_E_NOMEM, "output", e);
+      if (int r = unlz4_reserve_out(c, c->unFrame.as<uint8_t>(), fl, &size, &keep)) return r;
       if (int r = unlz4_decode(c, c->unFrame.as<uint8_t>(), fl, dl ? c->unDict.as<uint8_t>() : nullptr, dl,
                                c->unOut.as<uint8_t>(), keep, nullptr))
         return r;
@@ -1288,13 +1307,14 @@ int sz4_create(sz4_ctx** ctx, int device, uint64_t reserve_bytes)
   DeviceGuard guard(device);
   sz4_ctx* c = new sz4_ctx();
   c->device = device;
-  const char* sep = getenv("SZ4_SEPARATE_SORT");
-  c->separateSort = sep && sep[0] == '1';
   // tuning knobs (A/B): the batch API's piece size and the stream path's chunk size in bytes
   // (sz4_set_batch_chunk / sz4_set_stream_chunk set them per context)
   if (const char* bc = getenv("SZ4_BATCH_CHUNK")) {
     const uint64_t v = strtoull(bc, nullptr, 10);
-    if (v >= (1u << 20)) c->batchChunk = v;
+    if (v >= (1u << 20)) {
+      c->batchChunk = v;
+      c->batchChunkSet = true;
+    }
   }
   if (const char* sc = getenv("SZ4_STREAM_CHUNK")) {
     const uint64_t v = strtoull(sc, nullptr, 10);
@@ -1443,12 +1463,24 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
   // bounded memory: whole blocks in pieces of at most batchChunk input bytes, one pipeline run each
   // (the scratch is ~60-75 bytes per input byte), written one after the other into d_out
   // under a device bound the pieces shrink with it (the scratch is 36-60 bytes per piece byte)
+  // Without a bound the default piece is capped so that its scratch (< kScratchPerByte per piece byte) takes at
+  // most a quarter of the memory this context could use now (free + what it holds): a GPU shared with a
+  // caching allocator gets smaller pieces instead of SZ4_E_NOMEM.  A piece whose reservation still fails is
+  // halved and retried, down to kPieceFloor
   uint64_t chunk = c->batchChunk;
-  if (c->budget.limit) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(16ull << 20, c->budget.limit / 64));
-  const uint64_t piece = std::max<uint64_t>(block_size, chunk / block_size * block_size);
+  if (c->budget.limit) {
+    chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(kPieceFloor, c->budget.limit / 64));
+  } else if (!c->batchChunkSet) {
+    size_t freeB = 0, totalB = 0;
+    if (hipMemGetInfo(&freeB, &totalB) == hipSuccess)
+      chunk = std::min<uint64_t>(chunk, std::max<uint64_t>(kPieceFloor, (freeB + c->budget.used) / (4 * kScratchPerByte)));
+    else
+      (void)hipGetLastError();
+  }
+  uint64_t piece = std::max<uint64_t>(block_size, chunk / block_size * block_size);
   float stageSum[kStages] = {};
   uint64_t pos = 0;
-  if (n > piece) c->hostBytes.clear();
+  c->hostBytes.clear();
   for (uint64_t off = 0; off < n; off += piece) {
     const uint64_t len = std::min(piece, n - off);
     const bool firstPiece = off == 0, lastPiece = off + len == n;
@@ -1469,9 +1501,17 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
       c->planBS = block_size;
       c->streamPlanKey[0] = ~0ull;  // invalidate the stream path's plan cache
     }
-    if (int r = reserve_all(c, len + kPad)) return r;
-    hipError_t e;
-    if ((e = c->staged.reserve(len + kPad))) return c->fail(SZ4_E_NOMEM, "staging", e);
+    hipError_t e = hipSuccess;
+    int rr = reserve_all(c, len + kPad);
+    if (rr == SZ4_OK && (e = c->staged.reserve(len + kPad))) rr = c->fail(SZ4_E_NOMEM, "staging", e);
+    if (rr == SZ4_E_NOMEM && piece > block_size && piece > kPieceFloor) {
+      // smaller pieces: the next iteration re-plans this offset with half the piece
+      piece = std::max<uint64_t>(block_size, std::max<uint64_t>(kPieceFloor, piece / 2) / block_size * block_size);
+      c->planN = ~0ull;
+      off -= piece;  // the loop adds it back
+      continue;
+    }
+    if (rr) return rr;
     // private padded copy: kernels read 4-byte windows that may run past the caller's buffer
     if ((e = hipMemcpyAsync(c->staged.p, (const uint8_t*)d_in + off, len, hipMemcpyDeviceToDevice, s)))
       return c->fail(SZ4_E_DEVICE, "stage input", e);
@@ -1482,7 +1522,7 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
       return r;
     pos += size;
     for (int i = 0; i < kStages; i++) stageSum[i] += c->stageMs[i];
-    if (n > piece) {
+    if (!(firstPiece && lastPiece)) {
       // every piece's block sizes, for sz4_last_block_sizes
       const uint32_t nb = (uint32_t)c->hBlocks.size();
       const size_t at = c->hostBytes.size();
@@ -1491,7 +1531,7 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
         return c->fail(SZ4_E_DEVICE, "block sizes", e);
     }
   }
-  c->batchChunked = n > piece;
+  c->batchChunked = !c->hostBytes.empty();
   if (c->timing)
     for (int i = 0; i < kStages; i++) c->stageMs[i] = stageSum[i];
   *out_size = pos;
@@ -1549,7 +1589,10 @@ void sz4_set_stream_chunk(sz4_ctx* c, uint64_t bytes)
 
 void sz4_set_batch_chunk(sz4_ctx* c, uint64_t bytes)
 {
-  if (c) c->batchChunk = bytes ? bytes : kBatchChunkDefault;
+  if (c) {
+    c->batchChunk = bytes ? bytes : kBatchChunkDefault;
+    c->batchChunkSet = bytes != 0;
+  }
 }
 
 int sz4_last_stage_ms(sz4_ctx* c, float* stage_ms, int n)
@@ -1621,7 +1664,7 @@ int sz4_unlz4(sz4_ctx* c, const void* frame, uint64_t frame_len, const void* dic
   *out_size = total;
   if (total > out_cap || (total && !out)) return c->fail(SZ4_E_CAPACITY, "output buffer too small");
   if (!total) return SZ4_OK;
-  if ((e = c->unOut.reserve(total))) return c->fail(SZ4_E_NOMEM, "output", e);
+  if (int r = unlz4_reserve_out(c, c->unFrame.as<uint8_t>(), frame_len, &total, &keep)) return r;
   if (int r = unlz4_decode(c, c->unFrame.as<uint8_t>(), frame_len, dl ? c->unDict.as<uint8_t>() : nullptr, dl,
                            c->unOut.as<uint8_t>(), keep, nullptr))
     return r;

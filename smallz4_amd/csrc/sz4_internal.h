@@ -93,15 +93,11 @@ constexpr uint32_t kTokLast = 0x80000000u;
 
 // kernels (sz4_kernels.hip)
 uint32_t find_lds_bytes();
-uint32_t find_hybrid_lds_max();  // LDS for k_find_long9's [w0, s1 + 64) staging when the block is larger
 void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Interval* iv, uint32_t* ivCount,
                  hipStream_t s);
-void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks,
-                 const Interval* iv, const uint32_t* ivCount, uint2* elemA, uint2* elemB,
-                 uint32_t* rank, hipStream_t s);
-// pass 1 = k_find_sorted, pass 2 = k_find (long matches and shortcut intervals); fuseSort: pass 1 runs
-// k_sort's work for its segment first (compact = sorted slot arrays, scratch = sort buffer, rank written)
-// scratch: per-slot words free after k_sort (the skip pointers of k_find_long9); longBits: one bit per
+// pass 1 = k_find_sorted (each segment sorted first inside it: compact = sorted slot arrays, scratch = sort
+// buffer, rank written), pass 2 = k_find_big / k_find_long9 / k_find (long matches and shortcut intervals)
+// scratch: per-slot words free after the sort (the skip pointers of k_find_long9); longBits: one bit per
 // position marked for pass 2 (searched, not a shortcut interval); segLong: per segment, any such target;
 // specLen/specDist: per position words free before the parse (k_find_big's left-maximal results, then the
 // speculative carries of pass-2 piece heads); segTail: per segment, k_find_big's state after its last target
@@ -109,7 +105,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                  const Interval* iv, const uint32_t* ivCount, uint2* compact, uint2* scratch,
                  uint32_t* rank, uint32_t maxChain, uint32_t* mlen, uint16_t* mdist, uint64_t matchBase,
                  uint32_t* longBits, uint32_t* segLong, uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist,
-                 uint64_t* segTail, bool ldsWindow, uint32_t hybridLds, bool fuseSort, hipStream_t s);
+                 uint64_t* segTail, bool ldsWindow, hipStream_t s);
 // dictionary mode: one wavefront replays the reference's match loop (dictBack = first insertion offset
 // before the first block); last: 2^20 u32, prevH / prevX: 65536 u16 each -- the reference's tables,
 // kept in HBM between the chunks of one stream.  cont: the first block continues the stream of the
@@ -213,8 +209,17 @@ struct UnSub {
   uint32_t specFlags;        // 1: the walk met a malformed sequence at specExit, 2: it reached the block end
   uint32_t preN, specFrom;   // k_unlz4_fix: sequences re-parsed from the true entry, first speculative one kept
   uint32_t outRel, outLen;   // k_unlz4_fix: block-relative output offset and decoded bytes
-  uint32_t pad;
+  uint32_t specBytes;        // k_unlz4_spec: bytes its speculative list decodes
+  // k_unlz4_join: the join computed from an ASSUMED entry (the previous sub-segment's speculative exit):
+  // that entry, the exit it leads to, and 1: the previous walk was assumed to end there / 2: the join met a
+  // malformed sequence / 4: this sub-segment reaches the block end.  k_unlz4_fix keeps it where the
+  // assumption was the true chain's, and joins the others again from their true entry
+  uint32_t joinEntry, joinExit, joinFlags;
 };
+// per sub-segment, k_unlz4_spec's side tables (u32 words): the token-start mask (kUnSub / 32 words), the
+// mask's prefix bit counts per word (u16, kUnSub / 64 words), and each speculative sequence's output offset
+// from the sub-segment's first token (kUnSubCap words) -- k_unlz4_fix's rank and byte count in O(1)
+constexpr uint32_t kUnAuxWords = (kUnSub / 32 + kUnSub / 64 + kUnSubCap + 63) / 64 * 64;
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s);
 // the same result from the parallel index (candidate offsets, then one wavefront over their successors;
 // falls back to the serial walk in the same launch when the candidates cannot settle the chain)
@@ -229,13 +234,12 @@ void launch_unlz4_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb,
 void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint32_t nb, const uint4* seq, uint8_t* out,
                          const uint8_t* dict, uint64_t dl, uint32_t* flags, hipStream_t s);
 // split mode: seq holds 2 * kUnSubCap entries per sub-segment (re-parsed prefix, speculative list), masks
-// kUnSub / 32 words per sub-segment
+// kUnAuxWords words per sub-segment (the token-start mask and k_unlz4_spec's side tables)
 void launch_unlz4_split_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, UnSub* subs, uint32_t nsub,
                               uint4* seq, uint32_t* masks, hipStream_t s);
-// image: one u32 per output byte; flag: one u32 (any reference left after a resolve pass)
+// image: one u32 per output byte; hops: one u32 (zeroed before k_unlz4_pack: the longest reference chain it followed)
 void launch_unlz4_split_decode(const uint8_t* f, uint64_t n, const UnBlock* blk, const UnSub* subs, uint32_t nsub,
                                const uint4* seq, uint32_t* image, const uint8_t* dict, uint64_t dl, hipStream_t s);
-void launch_unlz4_resolve(uint32_t* image, uint64_t total, uint32_t* flag, hipStream_t s);
-void launch_unlz4_pack(const uint32_t* image, uint64_t total, uint8_t* out, hipStream_t s);
+void launch_unlz4_pack(uint32_t* image, uint64_t total, uint8_t* out, uint32_t* hops, hipStream_t s);
 
 }  // namespace sz4

@@ -2,11 +2,11 @@
 //
 // Pipeline per batch of blocks (all data resident in HBM):
 //   k_runs         same-letter runs -> shortcut intervals              (smallz4.h:631-643)
-//   k_sort         per segment: positions sorted by (4-byte key hash, position); replaces the
-//                  previousHash/previousExact chains                   (smallz4.h:645-720)
-//   k_find_sorted  pass 1, lane = target in sorted order: longest match over its key group
+//   k_find_sorted  per segment, first the sort of its positions by (4-byte key hash, position), which
+//                  replaces the previousHash/previousExact chains      (smallz4.h:645-720)
+//                  then pass 1, lane = target in sorted order: longest match over its key group
 //                                                                      (smallz4.h:173-255)
-//   k_find_long9 / k_find   pass 2 in text order: long matches, big groups, shortcut intervals
+//   k_find_big / k_find_long9 / k_find   pass 2: big groups, long matches, shortcut intervals
 //   k_prep         never-searched tail positions
 //   k_lazy_*       greedy/lazy skip bookkeeping in parallel, shortcut intervals checked
 //                                                                      (smallz4.h:631-643, 726-744)
@@ -28,12 +28,6 @@
 #include "sz4_internal.h"
 #include "sz4_device.h"
 
-#ifndef SZ4_SPEC_ATTR
-#define SZ4_SPEC_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))  // 8 waves/SIMD (SGPR spills to lanes are cheap)
-#endif
-#ifndef SZ4_SHIFT_UNROLL
-#define SZ4_SHIFT_UNROLL 1
-#endif
 #ifndef SZ4_SKIP_SHIFT  // timing experiments only (results wrong): leave out a phase of k_find_sorted
 #define SZ4_SKIP_SHIFT 0
 #endif
@@ -43,40 +37,25 @@
 #ifndef SZ4_SKIP_SEARCH
 #define SZ4_SKIP_SEARCH 0
 #endif
-#ifndef SZ4_FILTER
-#define SZ4_FILTER 1  // -9: candidates pass a strict-improvement mask test first, the exact prefix only on a hit
-#endif
-#ifndef SZ4_SAT_THRESHOLD
-#define SZ4_SAT_THRESHOLD 1  // -9 flush: a queued candidate is extended only if it can beat the target's best
-#endif
-#ifndef SZ4_FILTER_UNROLL
-#define SZ4_FILTER_UNROLL 0  // two candidates per hit test in the filtered loops (neutral at one workgroup per CU)
-#endif
-#ifndef SZ4_LEAN_SHIFT
-#define SZ4_LEAN_SHIFT 1  // -9, no window test: the shift-register walk as a uniform trip count
-#endif
-#ifndef SZ4_BIG_OCC
-#define SZ4_BIG_OCC 1  // k_find_big at 8 waves per SIMD (64 VGPRs; above 64 KiB blocks only the targets in LDS)
-#endif
-#ifndef SZ4_LONG9_TAIL
-#define SZ4_LONG9_TAIL 1  // k_find_long9_hbm stages only the segment's targets in LDS (0: [w0, s1 + 64), A/B)
-#endif
-#ifndef SZ4_SCAN_DPP
-#define SZ4_SCAN_DPP 1  // 0: wavefront prefix scans by ds_bpermute instead of DPP row shifts + row broadcasts (A/B)
-#endif
-#ifndef SZ4_HBM_GLOBAL  // k_find_sorted_hbm reads the text from HBM/L2 (no LDS window): two workgroups per CU
-#define SZ4_HBM_GLOBAL 1
-#endif
-#if SZ4_HBM_GLOBAL
-#define SZ4_HBM_SGPR 80
-#else
-#define SZ4_HBM_SGPR 96
-#endif
-#ifndef SZ4_XCD_ORDER  // k_find_sorted_hbm: contiguous runs of segments per XCD (A/B: no gain, profiles/r03/r03j2)
-#define SZ4_XCD_ORDER 0
-#endif
 #ifndef SZ4_DIAG
 #define SZ4_DIAG 0  // diagnostic builds only: 3 = per-wave timeline of k_find_sorted in sz4_diag[]
+#endif
+// SZ4_Dn(statements): the statements in the SZ4_DIAG == n build only (tools/build_diag.sh n; 3: k_find_sorted's
+// per-wave counters, 5: k_find_long9's, 6: k_find_big's phase clocks, 7: k_dp_fix's repair counters)
+#if SZ4_DIAG == 3
+#define SZ4_D3(...) __VA_ARGS__
+#else
+#define SZ4_D3(...)
+#endif
+#if SZ4_DIAG == 5
+#define SZ4_D5(...) __VA_ARGS__
+#else
+#define SZ4_D5(...)
+#endif
+#if SZ4_DIAG == 7
+#define SZ4_D7(...) __VA_ARGS__
+#else
+#define SZ4_D7(...)
 #endif
 
 namespace sz4 {
@@ -276,7 +255,6 @@ __device__ __forceinline__ uint32_t wave_min_fast(uint32_t v)
 // dependent VALU steps instead of six ds_bpermute round trips
 __device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v)
 {
-#if SZ4_SCAN_DPP
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 1, 0xF, 0xF, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 2, 0xF, 0xF, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 4, 0xF, 0xF, false);
@@ -284,20 +262,10 @@ __device__ __forceinline__ uint32_t wave_incl_scan_add(uint32_t v)
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast15, 0xA, 0xF, false);
   v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast31, 0xC, 0xF, false);
   return v;
-#else
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += o;
-  }
-  return v;
-#endif
 }
 
 __device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v)
 {
-#if SZ4_SCAN_DPP
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 1, 0xF, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 2, 0xF, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowShr + 4, 0xF, 0xF, false));
@@ -305,15 +273,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_max(uint32_t v)
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast15, 0xA, 0xF, false));
   v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kRowBcast31, 0xC, 0xF, false));
   return v;
-#else
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d && o > v) v = o;
-  }
-  return v;
-#endif
 }
 
 // load that bypasses the vector L1 (sc1): for data this wavefront itself rewrote earlier in the
@@ -439,21 +398,20 @@ __global__ __launch_bounds__(256) void k_runs(const uint8_t* __restrict__ in, co
 }
 
 // ================================================================================================
-// k_sort: one 1024-thread workgroup per segment.  Groups the inserted positions of the window
-// [w0, s1) by their four key bytes, positions ascending inside a group: one stable LSD radix sort
-// over a 16-bit hash of the key (two 8-bit passes) on packed 32-bit elements
-// (hash << posBits | position - w0).  Different keys that share a hash land in the same group;
-// the searches compare the four key bytes themselves, so the candidate sets stay exact.  After
-// the sort, the candidates of target p are the same-key entries just below p's slot -- the
-// reference's previousExact chain of p, nearest first.
-// Every pass goes through LDS a tile of kSortTile elements at a time: the tile is ranked (stable:
-// waves take consecutive sub-ranges, lanes rank by ballot), reordered by digit in LDS, and written
-// out as one contiguous run per digit -- whole cache lines instead of one scattered dword per
-// element.  The digit totals of both passes come from one histogram pass over the text, and pass 0
-// reads its keys straight from the text (no element array is written before it).
-// Outputs (in bufB, which the sort no longer needs): per slot the window position and the slot
-// where its hash group starts (u16 each when the window fits 16 bits, u32 otherwise).  The slot of a
-// target is written by k_find_sorted for the targets it hands to pass 2 only.
+// The sort (sort_segment, at the start of k_find_sorted): one 1024-thread workgroup per segment groups
+// the inserted positions of the window [w0, s1) by their four key bytes, positions ascending inside a
+// group.  Elements are packed 32-bit (hash << posBits | position - w0) with a 15/16-bit hash of the key;
+// different keys that share a hash land in the same group and the searches compare the four key bytes
+// themselves, so the candidate sets stay exact.  After the sort the candidates of target p are the
+// same-key entries just below p's slot -- the reference's previousExact chain of p, nearest first.
+// Stable MSD radix sort: one pass by the hash's high 8 bits through LDS, a tile of kSortTile elements at
+// a time (the tile ranked by ballot, reordered by digit in LDS, written out as one contiguous run per
+// digit: whole cache lines), its keys read straight from the text; then every high-digit bucket is sorted
+// by its low digit by one wavefront taken from a counter: low-digit counts by LDS atomics, whose exclusive
+// prefix is each hash group's start, and the elements ranked stably by ballot straight to their slots.
+// Outputs (in bufB): per slot the window position and the slot where its hash group starts (u16 each when
+// the window fits 16 bits, u32 otherwise).  The slot of a target is written by k_find_sorted for the
+// targets it hands to pass 2 only.
 // ================================================================================================
 constexpr int kSortThreads = 1024;
 constexpr int kSortWaves = kSortThreads / 64;
@@ -466,55 +424,14 @@ __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
   return (key * 2654435761u) >> posBits;  // top (32 - posBits) bits of a multiplicative hash
 }
 
-// k_sort's shared memory (57 KB).  When k_find_sorted sorts its own segment it lives in the window
-// buffer, which is loaded only after the sort.
-#ifndef SZ4_DP_BUMP
-#define SZ4_DP_BUMP 1  // 0: a fast chunk with a reachable literal-length bump finishes in the general loop
-#endif
-#ifndef SZ4_DP_VEC
-#define SZ4_DP_VEC 1  // 0: the parse's fast batches one position at a time in the scalar unit (A/B)
-#endif
 constexpr uint32_t kKeyNone = 0xFFFFFF00u;  // an invalid parse key that survives a +192 bias
 
-#ifndef SZ4_LEAN_SGPR
-#define SZ4_LEAN_SGPR 80  // k_dp_spec_lean's SGPR budget (80: 8 waves per SIMD, the rest spilled to VGPR lanes)
-#endif
-#ifndef SZ4_FIX_FORCED
-#define SZ4_FIX_FORCED 1  // 0: k_dp_fix walks a segment of forced same-letter matches chunk by chunk
-#endif
-#ifndef SZ4_BCAST_SAME
-#define SZ4_BCAST_SAME 1  // 0: the below-chunk broadcast reads and tests every candidate's three words
-#endif
-#ifndef SZ4_BCAST_DPP
-// 1: below-chunk candidates reach the lanes through DPP row_newbcast (16 replicated per register, VGPR-only
-// tests) instead of v_readlane into SGPRs: a VALU instruction with an SGPR operand issues at about 0.63x
-// the rate of one with VGPR operands only (tools/valu_ceiling.hip, profiles/valu_ceiling_r05.json)
-#define SZ4_BCAST_DPP 1
-#endif
-#ifndef SZ4_RUN_PREFIX
-#define SZ4_RUN_PREFIX 1  // 0: k_find extends candidates inside a same-letter run byte by byte (A/B)
-#endif
-#ifndef SZ4_BIG_INV
-#define SZ4_BIG_INV 1  // 0: k_find_big finds a run piece's place in its bucket by binary search (A/B)
-#endif
-#ifndef SZ4_LPF_BLOCK_MIN
-#define SZ4_LPF_BLOCK_MIN 65536  // LPF targets go to k_find_big only in blocks larger than this (A/B)
-#endif
-#ifndef SZ4_HIT2
-#define SZ4_HIT2 1  // 0: round 3's filter-hit code (masks from need bytes, satOk applied afterwards)
-#endif
-
-#ifndef SZ4_WALK_VEC
-#define SZ4_WALK_VEC 1  // 0: the forward walk one match at a time in the scalar unit (A/B)
-#endif
-
-#ifndef SZ4_MSD_SORT
-#define SZ4_MSD_SORT 1  // 0: two LSD passes through HBM and a group-start pass (A/B)
-#endif
+// The sort's shared memory (57 KB): k_find_sorted sorts its segment with it in the window buffer, which
+// is loaded only after the sort
 struct SortLds {
   uint32_t tile[kSortTile];        // a tile in digit order; the histogram pass's second table; the scan
   uint32_t cnt[kSortWaves][256];   // per wave and digit: count, then offset inside the tile
-  uint32_t gOff[2][256];           // per pass and digit: next output slot
+  uint32_t gOff[256];              // per high digit: next output slot
   uint32_t tileStart[256], tileCnt[256];
   uint64_t exLo[2 * kMaxIv], exHi[2 * kMaxIv];
   uint32_t wsum[kSortWaves];
@@ -583,11 +500,9 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     return (key_hash(gload4(in, q), pb) << pb) | r;
   };
 
-  // 1. digit totals of both passes: per-wave histograms (cnt: pass 0, tile: pass 1), then offsets
-  for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) {
-    (&L.cnt[0][0])[i] = 0;
-    L.tile[i] = 0;
-  }
+  // 1. the high digit's totals: per-wave histograms, then every digit's first slot (its bucket's start)
+  const uint32_t sh = pb + 8u;
+  for (uint32_t i = tid; i < kSortWaves * 256; i += kSortThreads) L.tile[i] = 0;
   __syncthreads();
   for (uint32_t i0 = tid; i0 < E; i0 += kSortThreads * kSortBatch) {
     uint32_t e[kSortBatch];
@@ -595,106 +510,88 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     for (uint32_t u = 0; u < kSortBatch; u++) e[u] = i0 + u * kSortThreads < E ? elem_at(i0 + u * kSortThreads) : 0u;
 #pragma unroll
     for (uint32_t u = 0; u < kSortBatch; u++)
-      if (i0 + u * kSortThreads < E) {
-        atomicAdd(&L.cnt[wave][(e[u] >> pb) & 255u], 1u);
-        atomicAdd(&L.tile[wave * 256 + ((e[u] >> (pb + 8)) & 255u)], 1u);
-      }
+      if (i0 + u * kSortThreads < E) atomicAdd(&L.tile[wave * 256 + ((e[u] >> sh) & 255u)], 1u);
   }
   __syncthreads();
   {
-    uint32_t h0 = 0, h1 = 0;
+    uint32_t h = 0;
     if (tid < 256)
-      for (uint32_t w = 0; w < kSortWaves; w++) {
-        h0 += L.cnt[w][tid];
-        h1 += L.tile[w * 256 + tid];
-      }
-    digit_scan(h0, L.gOff[0], L.wsum);
-    digit_scan(h1, L.gOff[1], L.wsum);
+      for (uint32_t w = 0; w < kSortWaves; w++) h += L.tile[w * 256 + tid];
+    digit_scan(h, L.gOff, L.wsum);
   }
-
-  // 2. stable passes, each tile ranked and reordered in LDS.  LSD: the low digit, then the high one.
-  //    MSD: the high digit only (buckets of equal high digit, positions ascending), then every bucket
-  //    is sorted by its low digit by one wavefront (step 3)
-#if SZ4_MSD_SORT
-  if (tid < 256) L.bstart[tid] = L.gOff[1][tid];
+  if (tid < 256) L.bstart[tid] = L.gOff[tid];
   if (tid == 0) {
     L.bstart[256] = E;
     L.bnext = 0;
   }
-  constexpr uint32_t kPass0 = 1;
-#else
-  constexpr uint32_t kPass0 = 0;
-#endif
-  uint32_t* src = reinterpret_cast<uint32_t*>(bufB + S.elemOff);  // pass 1 reads what pass 0 wrote
-  for (uint32_t pass = kPass0; pass < 2; pass++) {
-    uint32_t* dst = reinterpret_cast<uint32_t*>((pass == 0 ? bufB : bufA) + S.elemOff);
-    const uint32_t sh = pb + 8u * pass;
-    const bool fromText = pass == kPass0;
-    for (uint32_t t0 = 0; t0 < E; t0 += kSortTile) {
-      const uint32_t tn = E - t0 < kSortTile ? E - t0 : kSortTile;
-      for (uint32_t d = tid; d < kSortWaves * 256; d += kSortThreads) (&L.cnt[0][0])[d] = 0;
-      __syncthreads();
-      // wave w ranks elements [t0 + w * 512, +512), 64 per batch; (element, digit, rank in the wave)
-      uint32_t e[kSortBatch], rk[kSortBatch];
-      const uint32_t wb = t0 + wave * (64 * kSortBatch);
+
+  // 2. the stable pass by the high digit (buckets of equal high digit, positions ascending), keys from the
+  //    text, a tile at a time ranked and reordered in LDS; every bucket is then sorted by its low digit by
+  //    one wavefront (step 3)
+  uint32_t* src = reinterpret_cast<uint32_t*>(bufA + S.elemOff);
+  for (uint32_t t0 = 0; t0 < E; t0 += kSortTile) {
+    const uint32_t tn = E - t0 < kSortTile ? E - t0 : kSortTile;
+    for (uint32_t d = tid; d < kSortWaves * 256; d += kSortThreads) (&L.cnt[0][0])[d] = 0;
+    __syncthreads();
+    // wave w ranks elements [t0 + w * 512, +512), 64 per batch; (element, digit, rank in the wave)
+    uint32_t e[kSortBatch], rk[kSortBatch];
+    const uint32_t wb = t0 + wave * (64 * kSortBatch);
 #pragma unroll
-      for (uint32_t u = 0; u < kSortBatch; u++) {
-        const uint32_t i = wb + 64 * u + lane;
-        e[u] = i < t0 + tn ? (fromText ? elem_at(i) : src[i]) : 0u;
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kSortBatch; u++) {
-        const uint32_t i = wb + 64 * u + lane;
-        const bool valid = i < t0 + tn;
-        const uint32_t d = (e[u] >> sh) & 255u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-          const uint64_t m = __ballot((d >> b) & 1);
-          peers &= ((d >> b) & 1) ? m : ~m;
-        }
-        rk[u] = 0;
-        if (valid) {
-          const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-          rk[u] = L.cnt[wave][d] + below;
-        }
-        // the lowest lane of each digit advances the wave's count (after every lane has read it)
-        const bool leader = valid && (peers & ((1ull << lane) - 1ull)) == 0;
-        if (leader) L.cnt[wave][d] += (uint32_t)__popcll(peers);
-      }
-      __syncthreads();
-      // tile layout: digit-major, waves in order inside a digit
-      uint32_t tc = 0;
-      if (tid < 256)
-        for (uint32_t w = 0; w < kSortWaves; w++) {
-          const uint32_t c = L.cnt[w][tid];
-          L.cnt[w][tid] = tc;
-          tc += c;
-        }
-      digit_scan(tc, L.tileStart, L.wsum);
-      if (tid < 256) {
-        L.tileCnt[tid] = tc;
-        const uint32_t st = L.tileStart[tid];
-        for (uint32_t w = 0; w < kSortWaves; w++) L.cnt[w][tid] += st;
-      }
-      __syncthreads();
-#pragma unroll
-      for (uint32_t u = 0; u < kSortBatch; u++) {
-        const uint32_t i = wb + 64 * u + lane;
-        if (i < t0 + tn) L.tile[L.cnt[wave][(e[u] >> sh) & 255u] + rk[u]] = e[u];
-      }
-      __syncthreads();
-      // one contiguous run per digit
-      for (uint32_t i = tid; i < tn; i += kSortThreads) {
-        const uint32_t v = L.tile[i];
-        const uint32_t d = (v >> sh) & 255u;
-        dst[L.gOff[pass][d] + (i - L.tileStart[d])] = v;
-      }
-      __syncthreads();
-      if (tid < 256) L.gOff[pass][tid] += L.tileCnt[tid];
-      __syncthreads();
+    for (uint32_t u = 0; u < kSortBatch; u++) {
+      const uint32_t i = wb + 64 * u + lane;
+      e[u] = i < t0 + tn ? elem_at(i) : 0u;
     }
-    src = dst;
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++) {
+      const uint32_t i = wb + 64 * u + lane;
+      const bool valid = i < t0 + tn;
+      const uint32_t d = (e[u] >> sh) & 255u;
+      uint64_t peers = __ballot(valid);
+#pragma unroll
+      for (int b = 0; b < 8; b++) {
+        const uint64_t m = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? m : ~m;
+      }
+      rk[u] = 0;
+      if (valid) {
+        const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        rk[u] = L.cnt[wave][d] + below;
+      }
+      // the lowest lane of each digit advances the wave's count (after every lane has read it)
+      const bool leader = valid && (peers & ((1ull << lane) - 1ull)) == 0;
+      if (leader) L.cnt[wave][d] += (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // tile layout: digit-major, waves in order inside a digit
+    uint32_t tc = 0;
+    if (tid < 256)
+      for (uint32_t w = 0; w < kSortWaves; w++) {
+        const uint32_t c = L.cnt[w][tid];
+        L.cnt[w][tid] = tc;
+        tc += c;
+      }
+    digit_scan(tc, L.tileStart, L.wsum);
+    if (tid < 256) {
+      L.tileCnt[tid] = tc;
+      const uint32_t st = L.tileStart[tid];
+      for (uint32_t w = 0; w < kSortWaves; w++) L.cnt[w][tid] += st;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t u = 0; u < kSortBatch; u++) {
+      const uint32_t i = wb + 64 * u + lane;
+      if (i < t0 + tn) L.tile[L.cnt[wave][(e[u] >> sh) & 255u] + rk[u]] = e[u];
+    }
+    __syncthreads();
+    // one contiguous run per digit
+    for (uint32_t i = tid; i < tn; i += kSortThreads) {
+      const uint32_t v = L.tile[i];
+      const uint32_t d = (v >> sh) & 255u;
+      src[L.gOff[d] + (i - L.tileStart[d])] = v;
+    }
+    __syncthreads();
+    if (tid < 256) L.gOff[tid] += L.tileCnt[tid];
+    __syncthreads();
   }
   // the sorted elements are in bufA; bufB receives the per-slot arrays
   const bool small = W <= 65536u;  // == compact_small(S)
@@ -702,7 +599,6 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
   uint16_t* gs16 = pos16 + E;
   uint32_t* pos32 = reinterpret_cast<uint32_t*>(bufB + S.elemOff);
   uint32_t* gs32 = pos32 + E;
-#if SZ4_MSD_SORT
   // 3. every high-digit bucket by one wavefront, taken from a counter: its low digits counted, their
   //    exclusive prefix is each hash group's start (no scan over the segment), and the elements (in
   //    position order) are ranked stably by ballot, 64 at a time, straight to their final slots
@@ -770,55 +666,8 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     }
   }
   __syncthreads();
-#else
-  // 3. hash-group starts: tiles of 1024 consecutive slots, inclusive max-scan of (start slot + 1)
-  //    carried across tiles; every access coalesced
-  uint32_t* s_scan = L.tile;
-  uint32_t carry = 0;
-  // the next tile's element and its predecessor are loaded one tile ahead
-  uint32_t eN = tid < E ? src[tid] : 0u, pN = tid > 0 && tid < E ? src[tid - 1] : 0u;
-  for (uint32_t base = 0; base < E; base += kSortThreads) {
-    const uint32_t s = base + tid;
-    const bool valid = s < E;
-    const uint32_t e = eN, ep = pN;
-    const uint32_t sn = s + kSortThreads;
-    eN = sn < E ? src[sn] : 0u;
-    pN = sn < E ? src[sn - 1] : 0u;
-    const bool start = valid && (s == 0 || (e >> pb) != (ep >> pb));
-    uint32_t v = wave_incl_scan_max(start ? s + 1 : 0u);
-    if (lane == 63) s_scan[wave] = v;
-    __syncthreads();
-    uint32_t pre = carry;
-    for (uint32_t w = 0; w < wave; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
-    v = v > pre ? v : pre;
-    if (valid) {
-      const uint32_t g = v - 1u;
-      const uint32_t rel = e & posMask;
-      if (small) {
-        pos16[s] = (uint16_t)rel;
-        gs16[s] = (uint16_t)g;
-      } else {
-        pos32[s] = rel;
-        gs32[s] = g;
-      }
-    }
-    for (uint32_t w = wave; w < kSortWaves; w++) pre = s_scan[w] > pre ? s_scan[w] : pre;
-    carry = pre;
-    __syncthreads();
-  }
-#endif
 }
 
-__global__ __launch_bounds__(kSortThreads) void k_sort(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
-                                                       const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
-                                                       const uint32_t* __restrict__ ivCount, uint2* __restrict__ bufA,
-                                                       uint2* __restrict__ bufB)
-{
-  __shared__ SortLds lds;
-  const Segment S = segs[blockIdx.x];
-  const Block B = blocks[S.block];
-  sort_segment(in, S, B, ivAll, ivCount, bufA, bufB, lds);
-}
 
 // ================================================================================================
 // k_find: longest match per target position.  One workgroup per segment; wavefronts take chunks
@@ -843,24 +692,83 @@ struct Bytes<true> {
   const uint32_t* w;
   uint64_t base;
   __device__ __forceinline__ uint32_t ld4(uint64_t pos) const { return lload4(w, (uint32_t)(pos - base)); }
+  // bytes pos .. pos + 11 as three little-endian words
+  __device__ __forceinline__ void ld12(uint64_t pos, uint32_t& a, uint32_t& b, uint32_t& c) const
+  {
+    a = ld4(pos);
+    b = ld4(pos + 4);
+    c = ld4(pos + 8);
+  }
+  // bytes pos .. pos + 15 (reads up to pos + 19)
+  __device__ __forceinline__ void ld16(uint64_t pos, uint32_t (&v)[4]) const
+  {
+    const uint32_t off = (uint32_t)(pos - base), i = off >> 2, sh = off & 3;
+    const uint32_t w0 = w[i], w1 = w[i + 1], w2 = w[i + 2], w3 = w[i + 3], w4 = w[i + 4];
+    v[0] = __builtin_amdgcn_alignbyte(w1, w0, sh);
+    v[1] = __builtin_amdgcn_alignbyte(w2, w1, sh);
+    v[2] = __builtin_amdgcn_alignbyte(w3, w2, sh);
+    v[3] = __builtin_amdgcn_alignbyte(w4, w3, sh);
+  }
 };
 
 template <>
 struct Bytes<false> {
   const uint8_t* in;
   __device__ __forceinline__ uint32_t ld4(uint64_t pos) const { return gload4(in, pos); }
-};
-
-// the segment's targets and window staged in LDS, the rest of the block (long extensions) from HBM
-struct BytesHybrid {
-  const uint32_t* w;
-  uint64_t base, lim;  // LDS holds [base, lim)
-  const uint8_t* in;
-  __device__ __forceinline__ uint32_t ld4(uint64_t pos) const
+  // one 16-byte load (dword aligned; the staged input is padded) instead of three 8-byte ones: a third of
+  // the memory instructions and L2 requests for a candidate's or target's first 12 bytes
+  __device__ __forceinline__ void ld12(uint64_t pos, uint32_t& a, uint32_t& b, uint32_t& c) const
   {
-    return pos + 8 <= lim ? lload4(w, (uint32_t)(pos - base)) : gload4(in, pos);
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const u32x4a4 q = *reinterpret_cast<const u32x4a4*>(in + (pos & ~3ull));
+    const uint32_t sh = (uint32_t)(pos & 3);
+    a = __builtin_amdgcn_alignbyte(q.y, q.x, sh);
+    b = __builtin_amdgcn_alignbyte(q.z, q.y, sh);
+    c = __builtin_amdgcn_alignbyte(q.w, q.z, sh);
+  }
+  // bytes pos .. pos + 15: a 16-byte and a 4-byte load (reads up to pos + 19)
+  __device__ __forceinline__ void ld16(uint64_t pos, uint32_t (&v)[4]) const
+  {
+    typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+    const uint8_t* a = in + (pos & ~3ull);
+    const u32x4a4 q = *reinterpret_cast<const u32x4a4*>(a);
+    const uint32_t w4 = *reinterpret_cast<const uint32_t*>(a + 16);
+    const uint32_t sh = (uint32_t)(pos & 3);
+    v[0] = __builtin_amdgcn_alignbyte(q.y, q.x, sh);
+    v[1] = __builtin_amdgcn_alignbyte(q.z, q.y, sh);
+    v[2] = __builtin_amdgcn_alignbyte(q.w, q.z, sh);
+    v[3] = __builtin_amdgcn_alignbyte(w4, q.w, sh);
   }
 };
+
+// common prefix of the texts at x and y from byte k on (the first k known equal), at most cap: 16 bytes per
+// step -- the loads of a step are independent, one latency per 16 bytes of a long match instead of one per 4
+// -- while a whole step lies below cap, then 4 bytes per step (reading at most 3 bytes past cap, as before)
+template <class Src>
+__device__ __forceinline__ uint32_t ext_prefix(const Src& src, uint64_t x, uint64_t y, uint32_t k, uint32_t cap)
+{
+  while (k + 16 <= cap) {
+    uint32_t a[4], b[4];
+    src.ld16(x + k, a);
+    src.ld16(y + k, b);
+    const uint32_t d0 = a[0] ^ b[0], d1 = a[1] ^ b[1], d2 = a[2] ^ b[2], d3 = a[3] ^ b[3];
+    if (d0 | d1 | d2 | d3) {
+      const uint32_t j = d0 ? 0u : d1 ? 4u : d2 ? 8u : 12u;
+      const uint32_t d = d0 ? d0 : d1 ? d1 : d2 ? d2 : d3;
+      return k + j + ((uint32_t)__builtin_ctz(d) >> 3);
+    }
+    k += 16;
+  }
+  while (k < cap) {
+    const uint32_t d = src.ld4(x + k) ^ src.ld4(y + k);
+    if (d) {
+      k += (uint32_t)__builtin_ctz(d) >> 3;
+      break;
+    }
+    k += 4;
+  }
+  return k < cap ? k : cap;
+}
 
 // [base, base + span) in LDS, every other byte from HBM/L2 (positions below base included)
 struct BytesTail {
@@ -936,15 +844,9 @@ constexpr uint32_t kBigChunks = kLds ? 2048 : 4096;
 constexpr uint32_t kLongMatch = 0xFFFFFFFFu;
 constexpr uint32_t kBigGroup = 8192;  // -9: targets with more candidates go to k_find_big / k_find_long9
 constexpr uint32_t kBigRun = 2048;    // the same for a run key (vvvv) in blocks k_find_big takes
-#ifndef SZ4_BIG_RUN_L
-#define SZ4_BIG_RUN_L 32
-#endif
-#ifndef SZ4_LPF_MIN
-#define SZ4_LPF_MIN 256
-#endif
-constexpr uint32_t kBigRunL = SZ4_BIG_RUN_L;  // ... in blocks above 64 KiB (k_find_big's run table is exact and cheap)
-constexpr uint32_t kLpfMin = SZ4_LPF_MIN;     // ... and for an LPF target (below)
-constexpr uint32_t kLpfProbe = 8;
+constexpr uint32_t kBigRunL = 32;   // ... in blocks above 64 KiB (k_find_big's run table is exact and cheap)
+constexpr uint32_t kLpfMin = 256;   // ... and for an LPF target (below)
+constexpr uint64_t kLpfBlockMin = 65536;  // LPF targets go to k_find_big only in blocks larger than this
 __device__ __forceinline__ bool run_key(uint32_t k) { return k == (k & 0xFFu) * 0x01010101u; }
 // k_find_sorted's results leave in text order, tiles of kOutTile positions staged in LDS
 constexpr uint32_t kOutTileBits = 14;
@@ -953,7 +855,7 @@ constexpr uint32_t kOutTiles = 65536u / kOutTile;    // a segment has at most 65
 constexpr uint32_t kOutLong = 0xFFFFu;               // packed length: long, finished by pass 2
 constexpr uint32_t kOutUnsearched = 0xFFFEu;         // not a sorted target (shortcut interval)
 
-// per-slot arrays written by k_sort: u16 when the segment's window fits 16 bits (same predicate there)
+// per-slot arrays written by the sort: u16 when the segment's window fits 16 bits (same predicate there)
 __device__ __forceinline__ bool compact_small(const Segment& S) { return S.s1 - S.w0 <= 65536u; }
 __device__ __forceinline__ uint32_t slot_pos(const void* base, bool small, uint32_t s)
 {
@@ -964,42 +866,6 @@ __device__ __forceinline__ uint32_t slot_gs(const void* base, bool small, uint32
   return small ? (uint32_t)reinterpret_cast<const uint16_t*>(base)[E + s] : reinterpret_cast<const uint32_t*>(base)[E + s];
 }
 
-// An LPF target (k_find_big): a target whose candidates mostly share its
-// preceding byte -- records, markup, tables -- so that they carry from p-1 and k_find_big's
-// left-maximal search only visits the few others.  Decided on kLpfProbe candidates spread over the
-// group below the target: at least kLpfProbe - 2 of them share its preceding byte `cls`.
-#ifndef SZ4_LPF_LONG
-#define SZ4_LPF_LONG 0
-#endif
-constexpr uint32_t kLpfLong = SZ4_LPF_LONG;  // ... of which at least this many agree on all 12 key bytes
-#ifndef SZ4_LPF_LOCAL
-#define SZ4_LPF_LOCAL 1  // 0: the LPF routing decided by 8 probes into the group below the target (A/B)
-#endif
-#ifndef SZ4_LPF_SLACK
-#define SZ4_LPF_SLACK 1
-#endif
-constexpr uint32_t kLpfSlack = SZ4_LPF_SLACK;  // probes that may have another preceding byte
-template <class Src>
-__device__ __forceinline__ bool lpf_target(const void* compact, bool small, uint32_t gs, uint32_t slot, uint32_t cls,
-                                           uint64_t w0, uint64_t predLo, uint32_t me1, uint32_t me2, const Src& src)
-{
-  uint32_t same = 0, longer = 0;
-  for (uint32_t k = 0; k < kLpfProbe; k++) {
-    const uint64_t q = w0 + slot_pos(compact, small, gs + (uint32_t)((uint64_t)(slot - gs) * k / kLpfProbe));
-    same += q > predLo && (src.ld4(q - 1) & 0xFFu) == cls ? 1u : 0u;
-    if constexpr (kLpfLong > 0) longer += src.ld4(q + 4) == me1 && src.ld4(q + 8) == me2 ? 1u : 0u;
-  }
-  return same + kLpfSlack >= kLpfProbe && longer >= kLpfLong;
-}
-
-// workgroup i runs on XCD i mod 8 (observed, for speed only): XCD x's k-th workgroup takes segment
-// start(x) + k, so each XCD walks one contiguous run of segments
-__device__ __forceinline__ uint32_t xcd_segment(uint32_t i, uint32_t n)
-{
-  constexpr uint32_t kXcd = 8;
-  const uint32_t per = n / kXcd, extra = n % kXcd, x = i % kXcd, k = i / kXcd;
-  return x * per + (x < extra ? x : extra) + k;
-}
 
 template <bool kLds>
 __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
@@ -1007,7 +873,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
                                 const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
                                 uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
                                 uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
-                                uint32_t* rankOut, uint32_t fuseSort)
+                                uint32_t* rankOut)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
@@ -1017,13 +883,11 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   // exact key of each lane among them
   __shared__ uint32_t s_satQ[kFindThreads / 64][kSatQ];
   __shared__ uint32_t s_satBest[kFindThreads / 64][64];
-#if SZ4_DIAG == 3
-  const uint64_t tEntry = __builtin_readcyclecounter();
-#endif
+  SZ4_D3(const uint64_t tEntry = __builtin_readcyclecounter();)
   // blocks above 64 KiB: consecutive segments of a block share 64 KiB of window and their text comes
   // from HBM/L2 -- give each XCD a contiguous run of segments (workgroups are dealt round-robin over
   // the 8 XCDs, MI355X_MICROARCH.md "Workgroup dispatch"), so the runs stay in that XCD's L2
-  const uint32_t segIdx = (kLds || !SZ4_XCD_ORDER) ? blockIdx.x : xcd_segment(blockIdx.x, gridDim.x);
+  const uint32_t segIdx = blockIdx.x;
   const Segment S = segs[segIdx];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63;
@@ -1047,8 +911,8 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   }
   const uint32_t E = W - excluded;
   const bool small = compact_small(S);
-  if (fuseSort) {
-    // k_sort's work for this segment first, its shared memory in the (not yet loaded) window
+  {
+    // the sort of this segment first, its shared memory in the (not yet loaded) window
     // buffer: the latency-bound sort of one workgroup overlaps the issue-bound search of the other
     // workgroup on the CU, and the sorted slots it writes are read back while L2-warm
     sort_segment(in, S, B, ivAll, ivCount, sortA, compactAll, *reinterpret_cast<SortLds*>(win));
@@ -1061,25 +925,20 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   const uint32_t nTargets = (uint32_t)(S.s1 - S.s0);
   if (tid < kOutTiles) s_tileCnt[tid] = 0;
 
-#if SZ4_DIAG == 3
+  SZ4_D3(
   const uint64_t t0 = __builtin_readcyclecounter();
   uint64_t dB = 0, dL = 0, dBi = 0, dLi = 0;
-#endif
+  )
   if (tid == 0) {
     s_next = 0;
     s_long = 0;
   }
-  // kLds: the block's whole window in LDS; otherwise (SZ4_HBM_GLOBAL) every byte from HBM/L2, so that
+  // kLds: the block's whole window in LDS; otherwise (1) every byte from HBM/L2, so that
   // the LDS holds only the sort and the result tiles and two workgroups share a CU -- the candidates'
   // first 12 bytes live in registers, so text reads are per chunk and per extension, not per
   // candidate -- or [w0, s1 + 64) in LDS and the rest from HBM
-#if SZ4_HBM_GLOBAL
   typename std::conditional<kLds, Bytes<true>, Bytes<false>>::type src;
   if constexpr (kLds) {
-#else
-  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
-  {
-#endif
     const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
     const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
     for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
@@ -1090,9 +949,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       src.in = in;
     }
   }
-#if SZ4_HBM_GLOBAL
   if constexpr (!kLds) src.in = in;
-#endif
   __syncthreads();
 
   uint64_t cut = B.cut;
@@ -1125,8 +982,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     const uint32_t belowPre = slot_pos(compact, small, first > lane ? first - 1u - lane : 0u);
     const uint32_t gs = inChunk ? slot_gs(compact, small, E, slot) : slot;
     const uint64_t p = S.w0 + myRel;
-    const uint32_t me0 = inChunk ? src.ld4(p) : 0u, me1 = inChunk ? src.ld4(p + 4) : 0u;
-    const uint32_t me2 = inChunk ? src.ld4(p + 8) : 0u;
+    uint32_t me0, me1, me2;
+    src.ld12(p, me0, me1, me2);
+    if (!inChunk) me0 = me1 = me2 = 0u;
     const bool active = inChunk && p >= S.s0;  // window-only positions are candidates, not targets
     uint32_t room = 0, lbRel = 0, limit = 0;
     if (active) {
@@ -1146,8 +1004,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     const uint64_t predLoF = S.w0 > B.low ? S.w0 : B.low;
     // LPF targets in blocks above 64 KiB only: a 64 KiB block's groups are small, and text gains nothing
     // there that would pay for k_find_big's pass over the segment
-    const bool lpfBlock = B.end - B.start > (uint64_t)SZ4_LPF_BLOCK_MIN;
-#if SZ4_LPF_LOCAL
+    const bool lpfBlock = B.end - B.start > kLpfBlockMin;
     // the LPF decision from the chunk itself: a target of the group that began before the chunk (more than
     // kLpfMin members below it) whose preceding byte at least 3/4 of that group's lanes in the chunk share
     // (their positions are the group's nearest to the target) -- no probes into the group below
@@ -1165,32 +1022,22 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       }
       lpfLocal = cand && inGroup && nGroup >= 16u && (uint32_t)__popcll(peers) * 4u >= 3u * nGroup;
     }
-#endif
     const bool big = unlimited && cut == kNone && active &&
                      (slot - gs > kBigGroup ||
                       (lpfOk && ((run_key(me0) && slot - gs > (lpfBlock ? kBigRunL : kBigRun)) ||
-#if SZ4_LPF_LOCAL
                                  lpfLocal)));
-#else
-                                 (lpfBlock && slot - gs > kLpfMin && p > predLoF &&
-                                  lpf_target(compact, small, gs, slot, src.ld4(p - 1) & 0xFFu, S.w0, predLoF, me1, me2, src)))));
-#endif
     bool isLong = big, run = active && !big && bestLen < room && gs < slot;
     // a candidate improves iff its first need = bestLen + 1 bytes match: masks over bytes 4..11
     uint32_t m1 = 0, m2 = 0;
     // the candidate at cpos passed the mask test: its exact prefix (extended past 12 from the text)
     auto improve = [&](uint64_t cpos, uint32_t k1, uint32_t k2) {
-#if SZ4_DIAG == 3
-      dBi++;
-#endif
+      SZ4_D3(dBi++;)
       const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
       uint32_t kk = x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3) : 12u;
       if (kk == 12u) {
         bool open = true;
         while (open && kk < limit) {
-#if SZ4_DIAG == 3
-          dLi++;
-#endif
+          SZ4_D3(dLi++;)
           const uint32_t x = src.ld4(p + kk) ^ src.ld4(cpos + kk);
           if (x) {
             kk += (uint32_t)__builtin_ctz(x) >> 3;
@@ -1224,7 +1071,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // key = prefix << 17 | position (window-relative), order-free and branch-free.  Prefixes are exact
       // up to 12 bytes; candidates reaching 12 are queued and
       // extended from the text in batches of 64 (one per lane).
-      uint32_t bestKey = SZ4_HIT2 ? 3u << 17 : 0u;  // length 3: no match yet
+      uint32_t bestKey = 3u << 17;  // length 3: no match yet
       uint32_t qn = 0;
       bool walk = false;  // phase 1: this lane still takes candidates inside the chunk
       satBest[lane] = 0;
@@ -1240,9 +1087,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       auto flush = [&]() {
         // lane t extends queue entry base + t: target = lane (e >> 17), candidate position e & 0x1FFFF
         for (uint32_t base = 0; base < qn; base += 64) {
-#if SZ4_DIAG == 3
-        dLi += 1ull << 30;  // flush rounds
-#endif
+        SZ4_D3(dLi += 1ull << 30;)  // flush rounds
         const uint32_t e = base + lane < qn ? satQ[base + lane] : 0u;
         const uint32_t tl = e >> 17, cs = e & 0x1FFFFu;
         const uint32_t tRel = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(tl << 2), (int)myRel);
@@ -1251,7 +1096,6 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const uint64_t tp = S.w0 + tRel, cp = S.w0 + cs;
           uint32_t kk = 12;
           bool open = true;
-#if SZ4_SAT_THRESHOLD
           // queued after the target's best so far (nearest first), so it only counts if longer: it
           // must match byte `cur` (one 4-byte test) before it is extended
           const uint32_t cur = satBest[tl] >> 17;
@@ -1259,20 +1103,23 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             open = false;
             kk = 0;
           }
-#endif
-          while (open && kk < tLim) {
-#if SZ4_DIAG == 3
-            dLi++;  // lane-steps of the saturated extension
-#endif
-            const uint32_t x = src.ld4(tp + kk) ^ src.ld4(cp + kk);
-            if (x) {
-              kk += (uint32_t)__builtin_ctz(x) >> 3;
-              open = false;
-            } else {
-              kk += 4;
+          if constexpr (!kLds) {
+            // text from HBM/L2: 16 bytes per step (one load latency per step, not per 4 bytes)
+            if (open) kk = ext_prefix(src, tp, cp, 12u, tLim);
+          } else {
+            // the window in LDS: 4 bytes per step (the 16-byte step costs the LDS kernel spilled registers)
+            while (open && kk < tLim) {
+              SZ4_D3(dLi++;)  // lane-steps of the saturated extension
+              const uint32_t x = src.ld4(tp + kk) ^ src.ld4(cp + kk);
+              if (x) {
+                kk += (uint32_t)__builtin_ctz(x) >> 3;
+                open = false;
+              } else {
+                kk += 4;
+              }
             }
+            if (kk > tLim) kk = tLim;
           }
-          if (kk > tLim) kk = tLim;
           if (kk) atomicMax(&satBest[tl], (kk << 17) | cs);
         }
         }
@@ -1331,11 +1178,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           if (qn >= 64) flush();
         }
       };
-#if SZ4_FILTER
       // candidates arrive nearest first (slots descend), so one can raise bestKey only with a longer
       // prefix: it must match the first bestLen + 1 bytes (all 12 once a lane holds 12 or its cap).
       // m1 / m2 mask bytes 4..11 of that need; the exact prefix is computed on a hit only
-#if SZ4_HIT2
       // bestKey starts at length 3 (no match): the bytes to test past the first four are 8 (len - 3),
       // all of them once len reaches the cap -- as 63 mask bits: bit 63 of x2:x1 untested, which only
       // lets a rare candidate through the filter whose exact prefix then does not count
@@ -1346,23 +1191,12 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         m1 = (uint32_t)mk;
         m2 = (uint32_t)(mk >> 32);
       };
-#else
-      auto setMasks = [&]() {
-        const uint32_t len = bestKey >> 17;
-        const uint32_t need = len >= cap12 ? 12u : max(len + 1u, 4u);  // 4..12
-        const uint64_t mk = need >= 12u ? ~0ull : (1ull << (8u * (need - 4u))) - 1ull;
-        m1 = (uint32_t)mk;
-        m2 = (uint32_t)(mk >> 32);
-      };
-#endif
       auto filt = [&](uint32_t k0, uint32_t k1, uint32_t k2) -> uint32_t {
         return (k0 ^ me0) | ((k1 ^ me1) & m1) | ((k2 ^ me2) & m2);
       };
       // the hit, from the candidate's words already xor-ed with the lane's own (x0 = 0: same first word)
       auto hitx = [&](bool mine, uint32_t cs, uint32_t x0, uint32_t x1, uint32_t x2) {
-#if SZ4_DIAG == 3
-        dBi++;  // hit branches (wave-level)
-#endif
+        SZ4_D3(dBi++;)  // hit branches (wave-level)
         // v_ffbl_b32 gives ~0u for 0, so min() takes x2 when x1 is 0 (no compare and select)
         const uint32_t z = min(ffbl(x1), 32u + min(ffbl(x2), 32u));
         const uint32_t lcp = min(4u + (z >> 3), cap12);
@@ -1381,18 +1215,10 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         }
       };
       auto hit = [&](bool mine, uint32_t cs, uint32_t k0, uint32_t k1, uint32_t k2) {
-#if SZ4_HIT2
         hitx(mine, cs, k0 ^ me0, k1 ^ me1, k2 ^ me2);
-#else
-        const uint32_t x = scoreIf(mine, cs, k0, k1, k2);
-        setMasks();
-        enqueue(__ballot(x == 0u) & satOk, cs);
-#endif
       };
       setMasks();
-#endif
       // 1. inside the chunk: shift register (after s shifts lane l holds slot first + l - s)
-#if SZ4_LEAN_SHIFT
       {
         // lane l has slot - max(gs, first) candidates inside the chunk (lanes below it), so the walk is a
         // uniform trip count (the longest of them) with a per-lane bound -- no per-step walk flags.  With a
@@ -1419,38 +1245,14 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         const uint32_t trips = SZ4_SKIP_SHIFT ? 0u : max(max(rdlane(rm, 0), rdlane(rm, 16)), max(rdlane(rm, 32), rdlane(rm, 48)));
         uint32_t r0 = me0, r1 = me1, r2 = me2;
         uint32_t s = 1;
-#if SZ4_FILTER
         // wave shift right by one, zero into lane 0 (bound_ctrl: no old value to set up)
         auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kWaveShr1, 0xF, 0xF, true); };
         if (!needWin) {
           // a source lane below the target's group holds another key (x0 != 0), so only the lanes that do
           // not run need a mask, folded into the first word's test
           const uint32_t dead = run ? 0u : ~0u;
-#if SZ4_FILTER_UNROLL
-          // two shifts per test (a hit keeps the first candidate's words)
-          for (; s + 1 <= trips; s += 2) {
-#if SZ4_DIAG == 3
-            dL += 2;
-#endif
-            r0 = shr1(r0);
-            r1 = shr1(r1);
-            r2 = shr1(r2);
-            const uint32_t ya = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
-            const uint32_t q0 = r0, q1 = r1, q2 = r2;
-            r0 = shr1(r0);
-            r1 = shr1(r1);
-            r2 = shr1(r2);
-            const uint32_t yb = ((r0 ^ me0) | dead) | ((r1 ^ me1) & m1) | ((r2 ^ me2) & m2);
-            if (__ballot(min(ya, yb) == 0u)) {
-              if (__ballot(ya == 0u)) hit(s <= myCnt, spos(s), q0, q1, q2);
-              if (__ballot(yb == 0u)) hit(s + 1u <= myCnt, spos(s + 1u), r0, r1, r2);
-            }
-          }
-#endif
           for (; s <= trips; s++) {
-#if SZ4_DIAG == 3
-            dL++;
-#endif
+            SZ4_D3(dL++;)
             r0 = shr1(r0);
             r1 = shr1(r1);
             r2 = shr1(r2);
@@ -1459,9 +1261,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           }
         } else {
           for (; s <= trips; s++) {
-#if SZ4_DIAG == 3
-            dL++;
-#endif
+            SZ4_D3(dL++;)
             r0 = shr1(r0);
             r1 = shr1(r1);
             r2 = shr1(r2);
@@ -1470,32 +1270,8 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             if (__ballot(y == 0u)) hit(s <= myCnt, spos(s), r0, r1, r2);
           }
         }
-#elif SZ4_SHIFT_UNROLL
-        // two shifts per step, one saturation test for the two (four would exceed 64 VGPRs: 8 waves/SIMD)
-        for (; s + 1 <= trips; s += 2) {
-#if SZ4_DIAG == 3
-          dL += 2;
-#endif
-          uint32_t xs[2];
-#pragma unroll
-          for (uint32_t u = 0; u < 2; u++) {
-            r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
-            r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
-            r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
-            const bool mine = s + u <= myCnt;
-            const uint32_t x = score(mine ? spos(s + u) : 0u, mine ? r0 : ~me0, r1, r2);
-            xs[u] = mine ? x : 0xFFFFFFFFu;
-          }
-          if (__ballot(min(xs[0], xs[1]) == 0u) & satOk) {
-#pragma unroll
-            for (uint32_t u = 0; u < 2; u++) enqueue(__ballot(xs[u] == 0u) & satOk, spos(s + u));
-          }
-        }
-#endif
         for (; s <= trips; s++) {
-#if SZ4_DIAG == 3
-          dL++;
-#endif
+          SZ4_D3(dL++;)
           r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
           r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
           r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
@@ -1503,36 +1279,13 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         }
         run = run && (int32_t)gs < (int32_t)first;
       }
-#else
-      {
-        const int32_t lo1 = (int32_t)(gs > first ? gs : first);
-        uint32_t rRel = myRel, r0 = me0, r1 = me1, r2 = me2;
-        int32_t cl = (int32_t)slot;
-        walk = run && (int32_t)slot > lo1;  // a lane at the chunk start has none inside
-        while (__ballot(walk)) {
-#if SZ4_DIAG == 3
-          dL++;
-#endif
-          rRel = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)rRel, kWaveShr1, 0xF, 0xF, false);
-          r0 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r0, kWaveShr1, 0xF, 0xF, false);
-          r1 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r1, kWaveShr1, 0xF, 0xF, false);
-          r2 = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r2, kWaveShr1, 0xF, 0xF, false);
-          cl--;
-          if (needWin && walk && rRel < lbRel) walk = run = false;
-          const bool mine = walk;
-          walk = walk && cl > lo1;
-          visit(mine, (uint32_t)cl, r0, r1, r2);
-        }
-        run = run && (int32_t)gs < (int32_t)first;
-      }
-#endif
       // 2. below the chunk: the group that started before it, one uniform candidate per step
       if (!SZ4_SKIP_BCAST && __ballot(run)) {
         const int32_t gsB = (int32_t)rdlane(gs, 0);
         // a chunk whose 64 targets share their first word (inside one wide key group)
         const uint32_t me0u = rdlane(me0, 0);
         // (the LDS-window kernel only: in k_find_sorted_hbm the loop costs the registers of a second workgroup per CU)
-        const bool sameMe0 = SZ4_BCAST_SAME && kLds && __ballot(me0 == me0u) == ~0ull;
+        const bool sameMe0 = 1 && kLds && __ballot(me0 == me0u) == ~0ull;
         int32_t cBase = (int32_t)first - 1;
         uint32_t nextBlk = cBase - (int32_t)lane >= gsB ? belowPre : 0u;
         while (cBase >= gsB && __ballot(run)) {
@@ -1541,11 +1294,10 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const int32_t cn = cBase - 64 - (int32_t)lane;
           nextBlk = cn >= gsB ? slot_pos(compact, small, (uint32_t)cn) : 0u;
           const uint64_t fp = S.w0 + fRel;
-          const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
+          uint32_t f0, f1, f2;
+          src.ld12(fp, f0, f1, f2);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
-#if SZ4_DIAG == 3
-          dLi += 1ull << 46;  // broadcast blocks
-#endif
+          SZ4_D3(dLi += 1ull << 46;)  // broadcast blocks
           if (needWin) {
             // the block's candidates inside this lane's window: positions descend with k, so they are
             // the first kc (a binary search over the block); a lane whose window ends here is done
@@ -1560,8 +1312,6 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             }
             const uint32_t kc = run ? a : 0u;
             int32_t k = 0;
-#if SZ4_FILTER
-#if SZ4_BCAST_DPP
             // 16 candidates per register, every row a copy (lane l: candidate q0 + (l & 15)); step K takes
             // candidate q0 + K to every lane by DPP row_newbcast:K folded into the xor with the lane's word
             for (int32_t q0 = 0; q0 < n; q0 += 16) {
@@ -1585,13 +1335,6 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
 #undef SZ4_BSTEP_W
             }
             k = n;
-#else
-            for (; k < n; k++) {
-              const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
-              if (__ballot((uint32_t)k < kc && filt(k0, k1, k2) == 0u)) hit((uint32_t)k < kc, rdlane(fRel, (uint32_t)k), k0, k1, k2);
-            }
-#endif
-#endif
             for (; k + 1 < n; k += 2) {
               const uint32_t xa = scoreIf((uint32_t)k < kc, rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
               const uint32_t xb = scoreIf((uint32_t)k + 1u < kc, rdlane(fRel, (uint32_t)k + 1u), rdlane(f0, k + 1),
@@ -1608,28 +1351,12 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             // no window test: every lane may take the candidate (only the group's lanes can match; a
             // lane finished at its cap cannot move: its queued candidates never beat the one it has)
             int32_t k = 0;
-#if SZ4_FILTER
-#if SZ4_FILTER_UNROLL
-            for (; k + 1 < n; k += 2) {
-#if SZ4_DIAG == 3
-              dB += 2;
-#endif
-              const uint32_t a0 = rdlane(f0, k), a1 = rdlane(f1, k), a2 = rdlane(f2, k);
-              const uint32_t b0 = rdlane(f0, k + 1), b1 = rdlane(f1, k + 1), b2 = rdlane(f2, k + 1);
-              const uint32_t ya = filt(a0, a1, a2), yb = filt(b0, b1, b2);
-              if (__ballot(min(ya, yb) == 0u)) {
-                if (__ballot(ya == 0u)) hit(true, rdlane(fRel, (uint32_t)k), a0, a1, a2);
-                if (__ballot(yb == 0u)) hit(true, rdlane(fRel, (uint32_t)k + 1u), b0, b1, b2);
-              }
-            }
-#endif
-#if SZ4_BCAST_DPP
             {
               // 16 candidates per register, every row a copy (lane l: candidate q0 + (l & 15)); step K takes
               // candidate q0 + K to every lane by DPP row_newbcast:K folded into the xor with the lane's word.
               // A chunk whose 64 targets share their first word tests only the candidates with that word
               // (the others cannot pass): one scalar bit test per candidate, x0 = 0
-              const bool same = SZ4_BCAST_SAME && kLds && sameMe0;
+              const bool same = 1 && kLds && sameMe0;
               const uint64_t todo64 = same ? __ballot((int32_t)lane < n && f0 == me0u) : 0ull;
               for (int32_t q0 = 0; q0 < n; q0 += 16) {
                 const uint32_t todo = (uint32_t)(todo64 >> q0) & 0xFFFFu;
@@ -1666,8 +1393,6 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
               }
               k = n;
             }
-#endif
-#if SZ4_BCAST_SAME
             if (kLds && sameMe0 && k < n) {
               // every lane holds the same first word: only the block's candidates with that word can pass,
               // visited nearest first by bit scan, two readlanes each
@@ -1675,27 +1400,19 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
               while (todo) {
                 const uint32_t kk = (uint32_t)__builtin_ctzll(todo);
                 todo &= todo - 1ull;
-#if SZ4_DIAG == 3
-                dB++;
-#endif
+                SZ4_D3(dB++;)
                 const uint32_t k1 = rdlane(f1, kk), k2 = rdlane(f2, kk);
                 if (__ballot((((k1 ^ me1) & m1) | ((k2 ^ me2) & m2)) == 0u)) hit(true, rdlane(fRel, kk), me0u, k1, k2);
               }
               k = n;
             }
-#endif
             for (; k < n; k++) {
-#if SZ4_DIAG == 3
-              dB++;
-#endif
+              SZ4_D3(dB++;)
               const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k);
               if (__ballot(filt(k0, k1, k2) == 0u)) hit(true, rdlane(fRel, (uint32_t)k), k0, k1, k2);
             }
-#endif
             for (; k + 1 < n; k += 2) {
-#if SZ4_DIAG == 3
-              dB += 2;
-#endif
+              SZ4_D3(dB += 2;)
               const uint32_t xa = score(rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
               const uint32_t xb = score(rdlane(fRel, (uint32_t)k + 1u), rdlane(f0, k + 1), rdlane(f1, k + 1), rdlane(f2, k + 1));
               if (__ballot(min(xa, xb) == 0u) & satOk) {
@@ -1704,9 +1421,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
               }
             }
             for (; k < n; k++) {
-#if SZ4_DIAG == 3
-              dB++;
-#endif
+              SZ4_D3(dB++;)
               visit(true, rdlane(fRel, (uint32_t)k), rdlane(f0, k), rdlane(f1, k), rdlane(f2, k));
             }
           }
@@ -1755,9 +1470,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
         uint32_t r0 = me0, r1 = me1, r2 = me2;
         auto shr1 = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kWaveShr1, 0xF, 0xF, true); };
         for (uint32_t sft = 1; sft <= trips; sft++) {
-#if SZ4_DIAG == 3
-          dL++;
-#endif
+          SZ4_D3(dL++;)
           r0 = shr1(r0);
           r1 = shr1(r1);
           r2 = shr1(r2);
@@ -1786,10 +1499,10 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
           const int32_t cn = cBase - 64 - (int32_t)lane;
           nextBlk = cn >= gsB ? slot_pos(compact, small, (uint32_t)cn) : 0u;
           const uint64_t fp = S.w0 + fRel;
-          const uint32_t f0 = src.ld4(fp), f1 = src.ld4(fp + 4), f2 = src.ld4(fp + 8);
+          uint32_t f0, f1, f2;
+          src.ld12(fp, f0, f1, f2);
           const int32_t n = cBase - gsB + 1 < 64 ? cBase - gsB + 1 : 64;
           int32_t k = 0;
-#if SZ4_BCAST_DPP
           {
             // as at -9: 16 candidates per register, every row a copy, candidate q0 + K to every lane by DPP
             // row_newbcast:K folded into the xor -- in order, nearest first, as the step count needs; with a
@@ -1830,12 +1543,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             if (kc < (uint32_t)n) run = false;
             k = n;
           }
-#endif
           if (!needWin) {
             for (; k + 4 <= n; k += 4) {
-#if SZ4_DIAG == 3
-              dB += 4;
-#endif
+              SZ4_D3(dB += 4;)
               uint32_t a0[4], a1[4], a2[4], t[4];
 #pragma unroll
               for (int u = 0; u < 4; u++) {
@@ -1853,9 +1563,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
             }
           }
           for (; k < n && __ballot(run); k++) {
-#if SZ4_DIAG == 3
-            dB++;
-#endif
+            SZ4_D3(dB++;)
             const uint32_t k0 = rdlane(f0, k), k1 = rdlane(f1, k), k2 = rdlane(f2, k), crel = rdlane(fRel, k);
             if (needWin && run && crel < lbRel) run = false;
             if (run && test(k0, k1, k2) == 0u) improve(S.w0 + crel, k1, k2);
@@ -1890,9 +1598,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     }
     if (unlimited && __ballot(active && isLong) && lane == 0) s_long = 1;
   }
-#if SZ4_DIAG == 3
-  const uint64_t tSearch = __builtin_readcyclecounter();
-#endif
+  SZ4_D3(const uint64_t tSearch = __builtin_readcyclecounter();)
   __syncthreads();
   if (tid == 0) segLong[segIdx] = s_long;
 
@@ -1935,7 +1641,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     }
     __syncthreads();
   }
-#if SZ4_DIAG == 3
+  SZ4_D3(
   const uint64_t t2 = __builtin_readcyclecounter();
   const uint64_t w = (uint64_t)blockIdx.x * (kFindThreads / 64) + (tid >> 6);
   {
@@ -1947,7 +1653,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
     uint64_t* d = sz4_diag + w * 8;
     d[0] = t0; d[1] = t2; d[2] = dB; d[3] = dL; d[4] = dBi; d[5] = dLi; d[6] = tEntry; d[7] = tSearch;
   }
-#endif
+  )
 }
 
 // two 16-wave workgroups per CU need 8 waves per SIMD: .sgpr_count <= 80 (800 SGPRs per SIMD, a wave takes
@@ -1958,26 +1664,23 @@ __global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(80)
                                 const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
                                 uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
                                 uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
-                                uint32_t* rankOut, uint32_t fuseSort)
+                                uint32_t* rankOut)
 {
-  find_sorted_body<true>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
+  find_sorted_body<true>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut);
 }
-__global__ __launch_bounds__(kFindThreads, 2) __attribute__((amdgpu_num_sgpr(SZ4_HBM_SGPR))) void k_find_sorted_hbm(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(8), amdgpu_num_sgpr(80))) void k_find_sorted_hbm(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                 const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                 const uint32_t* __restrict__ ivCount, uint2* compactAll, uint32_t maxChain,
                                 uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist, uint64_t matchBase,
                                 uint32_t* __restrict__ longBits, uint32_t* __restrict__ segLong, uint2* sortA,
-                                uint32_t* rankOut, uint32_t fuseSort)
+                                uint32_t* rankOut)
 {
-  find_sorted_body<false>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut, fuseSort);
+  find_sorted_body<false>(in, segs, blocks, ivAll, ivCount, compactAll, maxChain, mlen, mdist, matchBase, longBits, segLong, sortA, rankOut);
 }
 
-// (SZ4_FIND2_OCC: two workgroups per CU when the window fits LDS -- <= 64 VGPRs, <= 80 SGPRs)
-#ifndef SZ4_FIND2_OCC
-#define SZ4_FIND2_OCC 1
-#endif
+// (1: two workgroups per CU when the window fits LDS -- <= 64 VGPRs, <= 80 SGPRs)
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ4_FIND2_OCC ? 8 : 1), amdgpu_num_sgpr(SZ4_FIND2_OCC ? 80 : 102))) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(8), amdgpu_num_sgpr(80))) void k_find(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                        const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                        const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                        const uint32_t* __restrict__ rankAll, uint32_t maxChain,
@@ -1993,7 +1696,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
   const uint32_t* rank = rankAll + S.rankOff;
   const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
   const uint32_t niv = ivCount[S.block];
-  // number of sorted slots (window minus shortcut-interval positions), as in k_sort
+  // number of sorted slots (window minus shortcut-interval positions), as in the sort
   uint32_t E = (uint32_t)(S.s1 - S.w0);
   {
     const uint32_t ids[2] = {B.prev, S.block};
@@ -2059,7 +1762,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
     int64_t slot = 0;
     uint32_t carryLen = 0, carryDist = 0;
     uint32_t resLen = pass1Len, resDist = pass1Dist;  // lane rowBase+t holds the result of target first+rowBase+t
-    uint64_t runLo = 0, runHi = 0;  // the row's last same-letter run (SZ4_RUN_PREFIX)
+    uint64_t runLo = 0, runHi = 0;  // the row's last same-letter run (1)
     bool wantRun = false;
     int64_t runJump = -1;            // the highest slot of the row's group below runLo, for (jumpLo, jumpGs)
     uint64_t jumpLo = ~0ull;
@@ -2067,7 +1770,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
     // after a target's first step inside a run, the rest of the group's candidates inside the run match
     // exactly as far as the nearest one (the run's end): none can win, the walk jumps below the run
     auto run_jump = [&]() {
-      if (!(SZ4_RUN_PREFIX && p >= runLo && p < runHi && slot >= (int64_t)gsCur)) return;
+      if (!(1 && p >= runLo && p < runHi && slot >= (int64_t)gsCur)) return;
       if (S.w0 + slot_pos(compact, small, (uint32_t)slot) < runLo) return;
       if (jumpLo != runLo || jumpGs != gsCur) {
         int64_t a = (int64_t)gsCur, b = slot;  // largest s in [a, b] with position < runLo, else a - 1
@@ -2117,7 +1820,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
         } else if (!done) {
           key = src.ld4(p);
           room = (uint32_t)(stopAbs - p);
-          wantRun = SZ4_RUN_PREFIX && key == (key & 0xFFu) * 0x01010101u && !(p >= runLo && p < runHi);
+          wantRun = 1 && key == (key & 0xFFu) * 0x01010101u && !(p >= runLo && p < runHi);
           lb = p > kWindow ? p - kWindow : 0;
           if (cut != kNone && ref_hash(key) == cutHash && cut > lb) lb = cut;
           slot = (int64_t)rCur - 1;
@@ -2163,7 +1866,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
           }
         }
       }
-#if SZ4_RUN_PREFIX
       // a target that starts four equal bytes outside the row's cached run: the run's extent, forward to
       // the block's last searchable byte and backward to the window base, 64 bytes per step over the
       // row's 16 lanes (once per run and row)
@@ -2214,7 +1916,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
           runHi = hiF < stopAbs ? hiF : stopAbs;
         }
       }
-#endif
       // one step: 16 candidates of the row's key group, nearest first
       const bool act = live && !done;
       bool valid = false, exhausted = true;
@@ -2412,8 +2113,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     s_next = 0;
   }
   // kLds: the block's whole window in LDS; otherwise [w0, s1 + 64) in LDS and the rest from HBM, or
-  // (SZ4_LONG9_TAIL) only the segment's own [s0, s1 + 64): 64 KiB, two workgroups per CU
-#if SZ4_LONG9_TAIL
+  // (1) only the segment's own [s0, s1 + 64): 64 KiB, two workgroups per CU
   typename std::conditional<kLds, Bytes<true>, BytesTail>::type src;
   {
     const uint64_t lo = kLds ? S.w0 : S.s0;
@@ -2427,20 +2127,6 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       src.in = in;
     }
   }
-#else
-  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
-  {
-    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
-    const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
-    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
-    src.w = win;
-    src.base = S.w0;
-    if constexpr (!kLds) {
-      src.lim = S.w0 + 4ull * words;
-      src.in = in;
-    }
-  }
-#endif
   __syncthreads();
   const uint32_t ne = nEx;
   uint32_t E = (uint32_t)(S.s1 - S.w0);
@@ -2498,14 +2184,14 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     __syncthreads();
   }
 
-  // same-letter runs (SZ4_RUN_PREFIX): the wave's last run [runLo, runHi) of a target's byte (runHi capped
+  // same-letter runs (1): the wave's last run [runLo, runHi) of a target's byte (runHi capped
   // at the block's last searchable byte).  A candidate inside the target's run matches exactly up to the
   // run's end, so after the nearest such candidate none of the others can win: the walk jumps below the
   // run (the slot, cached per run and key group).  Without it a run makes the walk quadratic.
   uint64_t runLo = 0, runHi = 0, jumpLo = ~0ull;
   int32_t jumpSlot = -1, jumpGs = -1;
   auto run_of = [&](uint64_t p, uint32_t key) {  // wave-uniform
-    if (!SZ4_RUN_PREFIX || key != (key & 0xFFu) * 0x01010101u || (p >= runLo && p < runHi)) return;
+    if (!1 || key != (key & 0xFFu) * 0x01010101u || (p >= runLo && p < runHi)) return;
     const uint32_t pat = key;
     uint64_t hi = p;
     for (uint64_t k = 0;; k += 256) {
@@ -2539,7 +2225,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     runHi = hi < stopAbs ? hi : stopAbs;
   };
   auto run_prefix = [&](uint64_t p, uint64_t c, uint32_t room, bool& known) -> uint32_t {
-    known = SZ4_RUN_PREFIX && p >= runLo && p < runHi && c >= runLo;
+    known = 1 && p >= runLo && p < runHi && c >= runLo;
     const uint64_t e = runHi - p;
     return e < (uint64_t)room ? (uint32_t)e : room;
   };
@@ -2565,9 +2251,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
 
   // best match of target p (wave-uniform): carry (cLen, cDist), exact = the carry is p-1's maximum
   auto best_of = [&](uint64_t p, uint32_t cLen, uint32_t cDist, bool exact, uint32_t& bLen, uint32_t& bDist) {
-#if SZ4_DIAG == 5
-    if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[0], 1ull);
-#endif
+    SZ4_D5(if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[0], 1ull);)
     const uint32_t key = src.ld4(p);
     const uint32_t room = (uint32_t)(stopAbs - p);
     uint64_t lb = p > kWindow ? p - kWindow : 0;
@@ -2618,7 +2302,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     }
     // inside a run: the nearest unvisited candidate, when it lies in the run, is the best of the run's
     // candidates (all match up to the run's end; it is the nearest); the walk goes on below the run
-    if (SZ4_RUN_PREFIX && key == (key & 0xFFu) * 0x01010101u && p >= runLo && p < runHi && s >= gs) {
+    if (1 && key == (key & 0xFFu) * 0x01010101u && p >= runLo && p < runHi && s >= gs) {
       const uint64_t c0 = S.w0 + slot_pos(compact, small, (uint32_t)s);
       if (c0 >= runLo) {
         if (c0 >= lb) {
@@ -2635,9 +2319,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       }
     }
     while (s >= gs) {
-#if SZ4_DIAG == 5
-      if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[1], 1ull);
-#endif
+      SZ4_D5(if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[1], 1ull);)
       const int32_t sl = s - (int32_t)lane;
       const bool inG = sl >= gs;
       const uint64_t c = inG ? S.w0 + slot_pos(compact, small, (uint32_t)sl) : 0u;
@@ -2683,9 +2365,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
   // one target per lane (a speculative batch): the same result as best_of under the same carry,
   // each lane walking its own candidates (class runs jumped with skip pointers)
   auto best_lane = [&](uint64_t p, uint32_t cLen, uint32_t cDist, uint32_t& bLen, uint32_t& bDist) {
-#if SZ4_DIAG == 5
-    atomicAdd((unsigned long long*)&sz4_diag[2], 1ull);
-#endif
+    SZ4_D5(atomicAdd((unsigned long long*)&sz4_diag[2], 1ull);)
     const uint32_t key = src.ld4(p);
     const uint32_t room = (uint32_t)(stopAbs - p);
     const uint64_t lb = p > kWindow ? p - kWindow : 0;  // no lookback cut on this path
@@ -2706,9 +2386,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       const int32_t gs = (int32_t)slot_gs(compact, small, E, slot);
       int32_t sl = (int32_t)slot - 1;
       while (sl >= gs) {
-#if SZ4_DIAG == 5
-        atomicAdd((unsigned long long*)&sz4_diag[3], 1ull);
-#endif
+        SZ4_D5(atomicAdd((unsigned long long*)&sz4_diag[3], 1ull);)
         const uint64_t c = S.w0 + slot_pos(compact, small, (uint32_t)sl);
         if (c < lb) break;  // positions descend: everything farther is out of the window
         if (prune && pred_class(c) == pc) {
@@ -2720,9 +2398,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
         if (src.ld4(c) == key) {
           const uint32_t need = bestDist == 0u ? 4u : (dist < bestDist ? bestLen : bestLen + 1u);
           const uint32_t got = prefix_if_at_least(src, p, c, need < 4u ? 4u : need, room);
-#if SZ4_DIAG == 5
-          atomicAdd((unsigned long long*)&sz4_diag[7], (unsigned long long)((need > got ? need : got) / 4u + 1u));
-#endif
+          SZ4_D5(atomicAdd((unsigned long long*)&sz4_diag[7], (unsigned long long)((need > got ? need : got) / 4u + 1u));)
           if (got >= need && got != 0u && (got > bestLen || dist < bestDist)) {
             bestLen = got;
             bestDist = dist;
@@ -2803,9 +2479,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
       const uint32_t aLen = mlen[q0 - 1 - matchBase], aDist = mdist[q0 - 1 - matchBase];
       if (aLen == specLen[q0 - matchBase] && aDist == sd) continue;
       walk_stretch(q0, aLen, aDist, true);
-#if SZ4_DIAG == 5
-      if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[4], 1ull);
-#endif
+      SZ4_D5(if (lane_id() == 0) atomicAdd((unsigned long long*)&sz4_diag[4], 1ull);)
     }
     return;
   }
@@ -2823,7 +2497,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
     const uint32_t p1 = lane < cnt ? mlen[myIdx] : 0u;
     if (__ballot(p1 == kLongMatch) == 0) continue;
     const bool lg = lane < cnt && long_bit(p);
-#if SZ4_DIAG == 5
+    SZ4_D5(
     {
       const uint32_t nl = (uint32_t)__builtin_popcountll(__ballot(lane < cnt && p1 == kLongMatch && lg));
       const uint32_t ni = (uint32_t)__builtin_popcountll(__ballot(lane < cnt && p1 == kLongMatch && !lg));
@@ -2838,7 +2512,7 @@ __device__ __forceinline__ void find_long9_body(const uint8_t* __restrict__ in, 
         }
       }
     }
-#endif
+    )
     // marked but never sorted: shortcut-interval targets copy the predecessor's match, minus one
     if (lane < cnt && p1 == kLongMatch && !lg) {
       for (uint32_t k = 0; k < niv; k++)
@@ -2901,7 +2575,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(80))) 
 {
   find_long9_body<true>(SZ4_LONG9_PASS);
 }
-__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(SZ4_LONG9_TAIL ? 80 : 102))) void k_find_long9_hbm(SZ4_LONG9_ARGS)
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_num_sgpr(80))) void k_find_long9_hbm(SZ4_LONG9_ARGS)
 {
   find_long9_body<false>(SZ4_LONG9_PASS);
 }
@@ -2966,7 +2640,9 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
     }                                                                                             \
   } while (0)
 #define SZ4_D6C(k, v) atomicAdd((unsigned long long*)&sz4_diag[k], (unsigned long long)(v))
+#define SZ4_D6X(...) __VA_ARGS__
 #else
+#define SZ4_D6X(...)
 #define SZ4_D6(k) \
   do {            \
   } while (0)
@@ -2975,7 +2651,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* wsum, 
   } while (0)
 #endif
 template <bool kLds>
-__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ4_BIG_OCC ? 8 : 1), amdgpu_num_sgpr(SZ4_BIG_OCC ? 80 : 102))) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
+__global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(8), amdgpu_num_sgpr(80))) void k_find_big(const uint8_t* __restrict__ in, const Segment* __restrict__ segs,
                                                            const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                            const uint32_t* __restrict__ ivCount,
                                                            const uint2* __restrict__ compactAll, uint2* __restrict__ scratchAll,
@@ -3046,10 +2722,10 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
   }
   const bool small = compact_small(S);
 
-#if SZ4_DIAG == 6
+  SZ4_D6X(
   uint64_t d6t = __builtin_readcyclecounter();
   if (tid == 0 && !resolveOnly) SZ4_D6C(15, 1);
-#endif
+  )
   // 1. big groups: the groups of the targets pass 1 handed on (marked, distance 0), found through their
   //    slots (rank): their starts as a bitmap over the window's slots, collected in slot order, each
   //    group's end by a binary search over the group starts
@@ -3102,10 +2778,10 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
     }
     __syncthreads();
   }
-#if SZ4_DIAG == 6
+  SZ4_D6X(
   if (tid == 0 && ng == 0) SZ4_D6C(24, 1);
   if (tid == 0 && ng > kMaxBigGroups) SZ4_D6C(25, 1);
-#endif
+  )
   if (ng == 0 || ng > kMaxBigGroups) return;  // (more cannot fit a window; pass 2 would take them)
   const uint64_t stopAbs = B.end - kTailLiterals;
 
@@ -3113,7 +2789,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
   // the second launch only resolves: a segment's first big targets need its predecessor segment's
   // last results, final after the first launch
   if (!resolveOnly) {
-#if SZ4_BIG_OCC
   // two workgroups per CU (<= 64 VGPRs): blocks above 64 KiB stage only the segment's own targets
   // [s0, s1 + 64) in LDS, the 64 KiB below them come from HBM/L2
   typename std::conditional<kLds, Bytes<true>, BytesTail>::type src;
@@ -3129,20 +2804,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
       src.in = in;
     }
   }
-#else
-  typename std::conditional<kLds, Bytes<true>, BytesHybrid>::type src;
-  {
-    const uint64_t end = kLds ? B.end + 8 : (S.s1 + 64 < B.end + 8 ? S.s1 + 64 : B.end + 8);
-    const uint32_t words = (uint32_t)((end - S.w0 + 3) / 4);
-    for (uint32_t i = tid; i < words; i += kFindThreads) win[i] = gload4(in, S.w0 + 4ull * i);
-    src.w = win;
-    src.base = S.w0;
-    if constexpr (!kLds) {
-      src.lim = S.w0 + 4ull * words;
-      src.in = in;
-    }
-  }
-#endif
   const uint64_t predLo = S.w0 > B.low ? S.w0 : B.low;  // a predecessor below this is not known here
   // class of a window position: its preceding byte, or kClsNone when that is not a chain position
   // (then the position is always left-maximal)
@@ -3189,9 +2850,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
         other += src.ld4(S.w0 + slot_pos(compact, small, s)) != gKey ? 1u : 0u;
       if (other) atomicAdd(&s_mixed, other);
       __syncthreads();
-#if SZ4_DIAG == 6
-      if (tid == 0 && s_mixed) SZ4_D6C(17, 1);
-#endif
+      SZ4_D6X(if (tid == 0 && s_mixed) SZ4_D6C(17, 1);)
     }
     // (a group of mostly other keys goes to the class path)
     const bool runGroup = run_key(gKey) && s_mixed * 4u <= gb - ga;
@@ -3296,9 +2955,7 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
         __syncthreads();
       }
       if (bad) s_mixed = 1;
-#if SZ4_DIAG == 6
-      if (bad) SZ4_D6C(16, 1);
-#endif
+      SZ4_D6X(if (bad) SZ4_D6C(16, 1);)
       __threadfence_block();
       __syncthreads();
       //    the piece at the window's end: its run's end by wave 0, 256 bytes per step, jumping intervals
@@ -3336,12 +2993,10 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
       __syncthreads();
       SZ4_D6(2);
       if (tid == 0) SZ4_D6C(12, nRuns);
-#if SZ4_DIAG == 6
-      if (tid == 0 && !s_mixed && nRuns > (uint32_t)(S.s1 - S.s0)) SZ4_D6C(18, 1);
-#endif
+      SZ4_D6X(if (tid == 0 && !s_mixed && nRuns > (uint32_t)(S.s1 - S.s0)) SZ4_D6C(18, 1);)
       if (!s_mixed && nRuns <= (uint32_t)(S.s1 - S.s0)) {  // (BK holds one word per target position of the segment)
       // with at most half as many pieces, BK's upper half maps a piece to its place in its bucket
-      const bool invBk = SZ4_BIG_INV && nRuns <= nTg / 2;
+      const bool invBk = 1 && nRuns <= nTg / 2;
       // B. buckets by next byte
       for (uint32_t k = tid; k < nRuns; k += kFindThreads) atomicAdd(&s_cur[0][C[ga + k] >> 17], 1u);
       __syncthreads();
@@ -3457,16 +3112,11 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
             if (l >= limit) break;  // the longest there is; the nearer ones came first
           }
         };
-#if SZ4_DIAG == 6
-        uint64_t w6 = __builtin_readcyclecounter();
+        SZ4_D6X(uint64_t w6 = __builtin_readcyclecounter();)
         auto W6 = [&](int k) {
-          const uint64_t now = __builtin_readcyclecounter();
-          if (lane == 0) SZ4_D6C(k, now - w6);
-          w6 = now;
+          (void)k;
+          SZ4_D6X(const uint64_t now = __builtin_readcyclecounter(); if (lane == 0) SZ4_D6C(k, now - w6); w6 = now;)
         };
-#else
-        auto W6 = [&](int) {};
-#endif
         const uint32_t need = R < limit ? R : limit;
         int32_t wj = -1;       // a piece start's walk: next piece to look at when still open
         bool open = false;
@@ -3655,7 +3305,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
         r1a = ga + s_cls[e0 + 1];
       }
       uint32_t bestKey = 0;
-#if SZ4_BCAST_DPP
       // candidates arrive in no particular order (class by class), so the filter lets through those that
       // reach the current best length (ties are decided by position in the key), all 12 bytes once the
       // best has 12 or the cap
@@ -3667,7 +3316,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
         m1 = (uint32_t)mk;
         m2 = (uint32_t)(mk >> 32);
       };
-#endif
       {
         // both candidate ranges as one sequence, 64 per step; the next step's entries of C are loaded
         // while this step's are scanned (unconditionally, at a clamped index: a load under a branch would
@@ -3688,7 +3336,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
           const uint64_t cp = S.w0 + (inR ? cr : 0u);
           const uint32_t f0 = src.ld4(cp), f1 = src.ld4(cp + 4), f2 = src.ld4(cp + 8);
           const uint32_t n = tot - base < 64u ? tot - base : 64u;
-#if SZ4_BCAST_DPP
           // 16 candidates per register, every row a copy; step K takes candidate q0 + K to every lane by DPP
           // row_newbcast:K (VGPR operands only), the exact prefix only when the filter lets it through
           for (uint32_t q0 = 0; q0 < n; q0 += 16) {
@@ -3735,36 +3382,6 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
             SZ4_BIGSTEP(12) SZ4_BIGSTEP(13) SZ4_BIGSTEP(14) SZ4_BIGSTEP(15)
 #undef SZ4_BIGSTEP
           }
-#else
-          for (uint32_t j = 0; j < n; j++) {
-            const uint32_t ej = rdlane(ce, j), k0 = rdlane(f0, j), k1 = rdlane(f1, j), k2 = rdlane(f2, j);
-            const uint32_t c = ej & 0x1FFFFu;
-            const bool ok = act && c < pRel && c >= lbRel && (ej >> 17) != exCls && k0 == me0;
-            const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
-            const uint32_t z1 = (uint32_t)(__ffs(x1) - 1), z2 = (uint32_t)(__ffs(x2) - 1);
-            const uint32_t z = min(z1, 32u + min(z2, 32u));
-            uint32_t lcp = min(4u + (z >> 3), cap12);
-            if (ok && lcp == 12u && limit > 12u) {
-              // both share 12 bytes: the exact prefix, unless the 4 bytes ending at the current best
-              // length already differ (then it stays below the best and cannot win)
-              const uint64_t cc = S.w0 + c;
-              const uint32_t bl = bestKey >> 17;
-              bool open = !(bl > 12u && src.ld4(p + bl - 4u) != src.ld4(cc + bl - 4u));
-              while (open && lcp < limit) {
-                const uint32_t x = src.ld4(p + lcp) ^ src.ld4(cc + lcp);
-                if (x) {
-                  lcp += (uint32_t)__builtin_ctz(x) >> 3;
-                  open = false;
-                } else {
-                  lcp += 4;
-                }
-              }
-              if (lcp > limit) lcp = limit;
-            }
-            const uint32_t key = ok ? (lcp << 17) | c : 0u;
-            bestKey = key > bestKey ? key : bestKey;
-          }
-#endif
         }
       }
       if (act) {
@@ -3867,14 +3484,14 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(SZ
       }
       anyHead |= __ballot(inR && kind != 0u) != 0;
       bool rmq = false;
-#if SZ4_DIAG == 6
+      SZ4_D6X(
       if (phase == 1 && resolveOnly) {
         const uint32_t nb = (uint32_t)__builtin_popcountll(__ballot(inR && kind == 0u && !valid));
         if (lane == 0 && nb) SZ4_D6C(26, nb);
         const uint32_t nu = (uint32_t)__builtin_popcountll(__ballot(inR && kind == 2u));
         if (lane == 0 && nu) SZ4_D6C(27, nu);
       }
-#endif
+      )
       if (phase == 1 && inR && kind == 0u && valid) {
         const uint64_t p = S.s0 + i, idx = p - matchBase;
         const uint32_t len = (uint32_t)(v >> 16) > i ? (uint32_t)(v >> 16) - i : 0u;
@@ -3958,7 +3575,6 @@ __device__ __forceinline__ uint32_t rmq_key(uint32_t cost, int32_t top, int32_t 
 // instead of six ds_bpermute round trips (the parse's range-minimum stores are latency-exposed)
 __device__ __forceinline__ uint32_t wave_incl_scan_min(uint32_t v)
 {
-#if SZ4_SCAN_DPP
   constexpr int kId = (int)0xFFFFFFFFu;
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 1, 0xF, 0xF, false));
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowShr + 2, 0xF, 0xF, false));
@@ -3967,15 +3583,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan_min(uint32_t v)
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowBcast15, 0xA, 0xF, false));
   v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(kId, (int)v, kRowBcast31, 0xC, 0xF, false));
   return v;
-#else
-  const uint32_t lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t o = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d && o < v) v = o;
-  }
-  return v;
-#endif
 }
 
 // UP of the chunk [hi - cnt + 1, hi] (lane t = position hi - t, key kt).  The chunk lies inside one
@@ -4966,7 +4573,6 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
     // that could reach one continues in the general loop below
     uint32_t tFast = 0;
     if (cnt == 64u) {
-#if SZ4_DP_VEC
       if (__ballot(myL > 64u) == 0 && lits + 4u < litBump) {  // every length <= 64
         // Row-transposed batches.  The window is held as lane 16q + j = cost[i0 + 4j + 4 - q] << 6, so the
         // next batch's window is one DPP row shift with the four new costs entering lane 0 of their own
@@ -5029,7 +4635,6 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
           t = tb + 4u;
           if (tb + 4u < 64u && lits + 4u >= litBump) break;
         }
-#if SZ4_DP_BUMP
         // the rest of the chunk with a literal-length bump reachable: the literal term of the prefix minimum
         // costs one more from the position whose run length reaches litBump on (only the all-literal path
         // from the batch start can reach it: after a match the run restarts below 4 < 15)
@@ -5063,7 +4668,6 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
           }
           w = (uint32_t)__builtin_amdgcn_update_dpp((int)((cp << 6) + rowBias), (int)w, kRowShr + 1, 0xF, 0xF, false);
         }
-#endif
         tFast = t;
         // transposed -> natural: lane l = cost[i0 + 1 + l] is transposed lane 16 (3 - (l & 3)) + (l >> 2)
         win = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((16u * (3u - (lane & 3u))) + (lane >> 2)) << 2), (int)w);
@@ -5078,51 +4682,6 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
         }
         chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
       }
-#else
-      const uint32_t rowMax = row_max(myL);
-      const uint32_t cmax = max(max(rdlane(rowMax, 0), rdlane(rowMax, 16)), max(rdlane(rowMax, 32), rdlane(rowMax, 48)));
-      auto fast = [&](auto smallTag) -> uint32_t {
-        constexpr bool kSmall = decltype(smallTag)::value;  // every length <= 16: row 0 holds every candidate
-#pragma unroll
-        for (uint32_t t = 0; t < 64; t += 4) {
-          if (lits + 4u >= litBump) return t;
-          uint32_t nwin = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lane - 4u) << 2), (int)win);
-          uint32_t kv[4];
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const uint32_t Lr = rdlane(myL, t + (uint32_t)r);
-            kv[r] = lane + 1u + (uint32_t)r <= Lr ? win + kLen[r] : 0xFFFFFFFFu;
-          }
-          if constexpr (kSmall) {
-#pragma unroll
-            for (int r = 0; r < 4; r++) kv[r] = rdlane(row_min(kv[r]), 0);
-          } else {
-            wave_min4(kv);
-          }
-          uint32_t mcost[4];
-          const uint32_t lits0 = lits;
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            // a match wins ties; invalid keys decode to costs no literal path reaches
-            const uint32_t mc = kv[r] >> 6;
-            const uint32_t c = min(costNext + 1u, mc);
-            lits = c == mc ? 0u : lits + 1u;
-            costNext = c;
-            mcost[r] = c;
-            kvBuf = wrlane(kvBuf, kv[r], t + (uint32_t)r);
-            mcBuf = wrlane(mcBuf, c, t + (uint32_t)r);
-          }
-          litBump = lits != lits0 + 4u ? 15u : litBump;  // a match was taken
-#pragma unroll
-          for (int r = 0; r < 4; r++) nwin = wrlane(nwin, mcost[r] << 6, 3u - (uint32_t)r);
-          win = nwin;
-        }
-        return 64u;
-      };
-      if (cmax <= 16u) tFast = fast(std::integral_constant<bool, true>());
-      else if (cmax <= 64u) tFast = fast(std::integral_constant<bool, false>());
-      if (tFast) chain.valid = chain.pending = false;  // lengths <= 64: no chain continues through here
-#endif
     }
     for (uint32_t t = tFast; t < 64; t += 4) {
       const int32_t i0 = hi - (int32_t)t;
@@ -5291,18 +4850,11 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
       uint32_t *__restrict__ costAll, uint32_t *__restrict__ sel, uint32_t *__restrict__ reach,            \
       uint4 *__restrict__ segState, const uint32_t *__restrict__ longFlag, uint32_t *__restrict__ upAll,   \
       uint32_t *__restrict__ downAll
-__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4_LEAN_SGPR))) void k_dp_spec_lean(SZ4_DP_SPEC_ARGS)
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(80))) void k_dp_spec_lean(SZ4_DP_SPEC_ARGS)
 {
   dp_spec_body<false>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
-#ifndef SZ4_RMQ_SGPR
-#define SZ4_RMQ_SGPR 80  // k_dp_spec_rmq's SGPR budget (80: 8 waves per SIMD; 0: the compiler's, 106 -> 7 waves)
-#endif
-#if SZ4_RMQ_SGPR
-__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(SZ4_RMQ_SGPR))) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
-#else
-__global__ __launch_bounds__(64 * kSpecWaves) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
-#endif
+__global__ __launch_bounds__(64 * kSpecWaves) __attribute__((amdgpu_num_sgpr(80))) void k_dp_spec_rmq(SZ4_DP_SPEC_ARGS)
 {
   dp_spec_body<true>(blocks, dpSegs, ndp, mlen, mdist, matchBase, costAll, sel, reach, segState, longFlag, upAll, downAll);
 }
@@ -5326,20 +4878,10 @@ constexpr uint32_t kDpSideStride = kDpSide + kDpSideKeys;
 // ... but only in blocks of more than this many parse segments: in a short block the serial walk is
 // short too, while a range-minimum block's parallel repair reads long match ranges at every position it
 // takes (zeros/urandom, 256 KiB blocks: parse 36.3 ms per 268 MB with it, 10.9 ms without)
-#ifndef SZ4_PAR_RMQ_MIN
-#define SZ4_PAR_RMQ_MIN 64
-#endif
-constexpr uint32_t kParRmqMinSegs = SZ4_PAR_RMQ_MIN;
+constexpr uint32_t kParRmqMinSegs = 64;
 
-#ifndef SZ4_FIX_SGPR
-#define SZ4_FIX_SGPR 0  // k_dp_fix's SGPR budget (0: the compiler's)
-#endif
 template <bool kPar>
-#if SZ4_FIX_SGPR
-__global__ __launch_bounds__(64) __attribute__((amdgpu_num_sgpr(SZ4_FIX_SGPR))) void k_dp_fix(
-#else
 __global__ __launch_bounds__(64) void k_dp_fix(
-#endif
 const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
                                                uint32_t ndp, const uint32_t* __restrict__ mlen,
                                                const uint16_t* __restrict__ mdist,
@@ -5373,11 +4915,11 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
   const Block B = blocks[bIdx];
   if (B.dpCount <= 1) return;
   const uint32_t lane = threadIdx.x;
-#if SZ4_DIAG == 7
+  SZ4_D7(
   // k_dp_fix<false> per block: serial positions, closed-form chunks, literal chunks, segments walked
   uint64_t d7Serial = 0, d7Closed = 0, d7Lit = 0, d7Segs = 0;
   const uint64_t d7t0 = __builtin_readcyclecounter();
-#endif
+  )
   if constexpr (kPar) {
     // a segment without any match cannot converge (that needs a match): nothing written, k_dp_fix<false>
     // repairs it in closed form
@@ -5580,13 +5122,9 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
         lowW = cl;
       }
       closedRun = false;
-#if SZ4_DIAG == 7
-      if (h == hi) d7Segs++;
-#endif
+      SZ4_D7(if (h == hi) d7Segs++;)
       if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
-#if SZ4_DIAG == 7
-        d7Lit++;
-#endif
+        SZ4_D7(d7Lit++;)
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
         auto lit_cost = [&](uint32_t t, uint32_t& nb) -> uint32_t {
           const uint32_t run = lits + t + 1u;
@@ -5642,9 +5180,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
                    return false;
                  }()) {
         const uint32_t cT = closedCost + len_extra((uint32_t)(closedE - ip));
-#if SZ4_DIAG == 7
-        d7Closed++;
-#endif
+        SZ4_D7(d7Closed++;)
         if (closedE > maxReach) maxReach = closedE;
         if (closedE != chain.E) chain.valid = chain.pending = false;
         const uint32_t delta = cT - cC;
@@ -5654,7 +5190,6 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
         const int32_t rt = (chg & upTo) ? h - (63 - (int32_t)__builtin_clzll(chg & upTo)) : runTop;
         const int32_t need = (int32_t)cR > ip ? (int32_t)cR : ip;
         uint64_t cv = __ballot(lane < cnt && cS != 1u && rt >= need);
-#if SZ4_FIX_FORCED
         // every position from here down to the segment's bottom takes the same run's match unconditionally
         // (smallz4.h:409-415: length >= MaxSameLetter, distance 1, the same end): its choice is the stored
         // one and its cost the stored one plus this chunk's (constant) offset -- converged right here
@@ -5665,7 +5200,6 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
           }
           if (forcedOk) cv = 1ull;  // lane 0: position h
         }
-#endif
         const uint32_t last = cv ? (uint32_t)__builtin_ctzll(cv) : cnt - 1u;  // last position processed
         if (lane <= last) {
           S[ip] = cL;
@@ -5690,9 +5224,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
       for (uint32_t t = 0; t < 64; t++) {
         const int32_t i = h - (int32_t)t;
         if (i < lo) break;
-#if SZ4_DIAG == 7
-        d7Serial++;
-#endif
+        SZ4_D7(d7Serial++;)
         const uint32_t Lk = rdlane(cL, t), Dk = rdlane(cD, t);
         if (Lk >= (uint32_t)kMinMatch && i + (int32_t)Lk > maxReach) maxReach = i + (int32_t)Lk;
         lits++;
@@ -5813,7 +5345,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
       prevKeyLim = convBlk[k];
     }
   }
-#if SZ4_DIAG == 7
+  SZ4_D7(
   if (!kPar && lane == 0) {
     const uint64_t dt = __builtin_readcyclecounter() - d7t0;
     atomicAdd((unsigned long long*)&sz4_diag[0], (unsigned long long)d7Serial);
@@ -5826,7 +5358,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
     atomicAdd((unsigned long long*)&sz4_diag[7], 1ull);
     if (rmq) atomicAdd((unsigned long long*)&sz4_diag[8], 1ull);
   }
-#endif
+  )
 }
 
 // ================================================================================================
@@ -5859,7 +5391,6 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   const uint32_t a = ws.y * kWalkSeg;
   const uint32_t aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
 
-#if SZ4_WALK_VEC
   // A window of 64 positions at a time, on the vector unit: lane l steps to l + max(1, chosen[l])
   // (F1, 64 = out of the window), F2 .. F32 by doubling (ds_bpermute), and every lane finds the last
   // path position at or below itself by binary lifting from the entry; the lanes that find themselves
@@ -5921,74 +5452,6 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_walk(const Block* __restric
   }
   if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, exitPos, 0u);
 }
-#else
-  uint32_t pos = a, wbase = a, m = 0, slotBuf = 0;
-  bool viaMatch = false;
-  uint32_t wL, xL1, xL2, xL3;
-  // unconditional loads (the index clamped; lanes past the block are masked where the window is
-  // used): a load under a branch, or a value masked right after it, makes the compiler wait for the
-  // load before the window is used, which defeats the prefetch
-  auto ldw = [&](uint32_t b) -> uint32_t {
-    const uint32_t i = b + lane;
-    return L[i < n ? i : n - 1u];
-  };
-  wL = ldw(a);
-  xL1 = ldw(a + 64);
-  xL2 = ldw(a + 128);
-  xL3 = ldw(a + 192);
-  // per window, each lane's offset of the first match at or after it (64: none): computed once per
-  // window on the vector unit, so a step of the walk is two readlanes instead of a ballot and a bit scan
-  auto next_match = [&]() -> uint32_t {
-    const uint64_t ge = __ballot(wL > 1u && wbase + lane < n) & (~0ull << lane);
-    return ge ? (uint32_t)__builtin_ctzll(ge) : 64u;
-  };
-  uint32_t nm = next_match();
-  while (pos < aNext) {
-    if (pos >= wbase + 64) {
-      while (pos >= wbase + 64) {
-        if (pos < wbase + 256) {
-          wbase += 64;
-          wL = xL1;
-          xL1 = xL2;
-          xL2 = xL3;
-          xL3 = ldw(wbase + 192);
-        } else {
-          wbase = pos & ~63u;
-          wL = ldw(wbase);
-          xL1 = ldw(wbase + 64);
-          xL2 = ldw(wbase + 128);
-          xL3 = ldw(wbase + 192);
-        }
-      }
-      nm = next_match();
-    }
-    const uint32_t qr = rdlane(nm, pos - wbase);
-    const uint32_t q = wbase + qr;  // next match (or window end)
-    if (q >= aNext) {
-      viaMatch = false;  // literals carry the path to aNext itself
-      break;
-    }
-    if (qr == 64u) {
-      pos = q;
-      viaMatch = false;
-      continue;
-    }
-    if (m >= kWalkCap) {
-      // a match is at least kMinMatch long, so a sub-segment holds at most kWalkSeg / 4 + 1 of them
-      if (lane == 0) atomicOr(status, kStInvariant);
-      break;
-    }
-    // match positions collect in a register (lane m mod 64) and leave 64 at a time, coalesced
-    slotBuf = wrlane(slotBuf, q, m & 63u);
-    m++;
-    if ((m & 63u) == 0u) slots[m - 64u + lane] = slotBuf;
-    pos = q + rdlane(wL, qr);
-    viaMatch = true;
-  }
-  if (lane < (m & 63u)) slots[(m & ~63u) + lane] = slotBuf;
-  if (lane == 0) state[idx] = make_uint4(kWalkCap, kWalkCap + m, viaMatch ? pos : aNext, 0u);
-}
-#endif
 
 // Sub-segment repair.  Sub-segment k's walk is exact when the true path enters it at a position the
 // speculative walk also visits; otherwise the path is walked again from its true entry until it meets
@@ -6343,11 +5806,8 @@ __global__ __launch_bounds__(kAsmThreads) void k_block_bytes(const Block* __rest
   }
 }
 
-#ifndef SZ4_WRITE_WAVES
-#define SZ4_WRITE_WAVES 1  // k_write_seg's minimum waves per SIMD (launch bound): 1 leaves its registers free (77: 6 waves)
-#endif
 // one wavefront per sub-segment writes its tokens (or its raw bytes) into the frame
-__global__ __launch_bounds__(64 * kSegWaves, SZ4_WRITE_WAVES) void k_write_seg(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
+__global__ __launch_bounds__(64 * kSegWaves) void k_write_seg(const uint8_t* __restrict__ in, const Block* __restrict__ blocks,
                                                              const uint2* __restrict__ walkSegs, uint32_t nwalk,
                                                              const uint4* __restrict__ state, const uint4* __restrict__ info,
                                                              const Token* __restrict__ tokAll, const uint32_t* __restrict__ ntokAll,
@@ -6477,23 +5937,16 @@ void launch_runs(const uint8_t* in, const Block* blocks, uint32_t nblocks, Inter
   if (nblocks) hipLaunchKernelGGL(k_runs, dim3(nblocks), dim3(256), 0, s, in, blocks, iv, ivCount);
 }
 
-void launch_sort(const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
-                 const uint32_t* ivCount, uint2* elemA, uint2* elemB, uint32_t* rank, hipStream_t s)
-{
-  (void)rank;  // written by k_find_sorted for the targets pass 2 takes
-  if (nsegs) hipLaunchKernelGGL(k_sort, dim3(nsegs), dim3(kSortThreads), 0, s, in, segs, blocks, iv, ivCount, elemA, elemB);
-}
 
 uint32_t dp_side_positions() { return kDpSideStride; }
 
 uint32_t find_lds_bytes() { return 65536 + 16; }
-uint32_t find_hybrid_lds_max() { return 150u * 1024u; }
 
 void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nsegs, const Block* blocks, const Interval* iv,
                  const uint32_t* ivCount, uint2* compact, uint2* scratch, uint32_t* rank, uint32_t maxChain,
                  uint32_t* mlen, uint16_t* mdist, uint64_t matchBase, uint32_t* longBits, uint32_t* segLong,
                  uint32_t* longFlag, uint32_t* specLen, uint32_t* specDist, uint64_t* segTail, bool ldsWindow,
-                 uint32_t hybridLds, bool fuseSort, hipStream_t s)
+                 hipStream_t s)
 {
   static_assert(sizeof(SortLds) <= 65536, "the fused sort's shared memory must fit the window buffer");
   static_assert(kOutTile * 4u <= 65536u + 16u, "a result tile must fit the window buffer");
@@ -6507,15 +5960,13 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
     if (pass == 1)
       hipLaunchKernelGGL(k_find_sorted_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
-                         ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank,
-                         (uint32_t)fuseSort);
+                         ivCount, compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank);
     else if (unlimited) {
       // big key groups first (left-maximal candidates + text-order prefix maximum), then pass 2
       hipFuncSetAttribute((const void*)k_find_big<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)find_lds_bytes());
-      if (!getenv("SZ4_NO_BIG"))
-        for (uint32_t resolve = 0; resolve < 2; resolve++)
-          hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
+      for (uint32_t resolve = 0; resolve < 2; resolve++)
+        hipLaunchKernelGGL(k_find_big<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
+                           compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_lds, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv,
                            ivCount, compact, scratch, rank, longBits, segLong, mlen, mdist, matchBase, longFlag, specLen,
@@ -6526,21 +5977,20 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
   } else {
     if (pass == 1) {
       // the sort and the text-order result tiles use the same buffer: at least 64 KiB
-      const uint32_t lds = (hybridLds > kOutTile * 4u && !SZ4_HBM_GLOBAL) ? hybridLds : kOutTile * 4u;
+      const uint32_t lds = kOutTile * 4u;
       hipFuncSetAttribute((const void*)k_find_sorted_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(k_find_sorted_hbm, dim3(nsegs), dim3(kFindThreads), lds, s, in, segs, blocks, iv, ivCount,
-                         compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank, (uint32_t)fuseSort);
+                         compact, maxChain, mlen, mdist, matchBase, longBits, segLong, scratch, rank);
     }
     else if (unlimited) {
-      // (SZ4_BIG_OCC: the segment's own 64 Ki targets and 64 bytes more)
-      const uint32_t bigLds = SZ4_BIG_OCC ? 65536u + 256u : hybridLds;
+      // (the segment's own 64 Ki targets and 64 bytes more)
+      const uint32_t bigLds = 65536u + 256u;
       hipFuncSetAttribute((const void*)k_find_big<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bigLds);
-      if (!getenv("SZ4_NO_BIG"))
-        for (uint32_t resolve = 0; resolve < 2; resolve++)
-          hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), bigLds, s, in, segs, blocks, iv, ivCount,
-                             compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
-      // (SZ4_LONG9_TAIL: the segment's own 64 Ki targets and 64 bytes more)
-      const uint32_t l9Lds = SZ4_LONG9_TAIL ? 65536u + 256u : hybridLds;
+      for (uint32_t resolve = 0; resolve < 2; resolve++)
+        hipLaunchKernelGGL(k_find_big<false>, dim3(nsegs), dim3(kFindThreads), bigLds, s, in, segs, blocks, iv, ivCount,
+                           compact, scratch, longBits, segLong, mlen, mdist, matchBase, specLen, segTail, specDist, rank, longFlag, resolve);
+      // (the segment's own 64 Ki targets and 64 bytes more)
+      const uint32_t l9Lds = 65536u + 256u;
       hipFuncSetAttribute((const void*)k_find_long9_hbm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l9Lds);
       for (int fix = 0; fix < 2; fix++)
         hipLaunchKernelGGL(k_find_long9_hbm, dim3(nsegs), dim3(kFindThreads), l9Lds, s, in, segs, blocks, iv, ivCount,

@@ -5,7 +5,10 @@
 // precede the output (smallz4cat.c:168-187), legacy decoding ending after the first block shorter
 // than 8 MiB (smallz4cat.c:325-327).
 //
-//   k_unlz4_index   one lane walks the block size words (a dependent chain, smallz4cat.c:189-205)
+//   k_unlz4_ix_*    the block index (the chain of size words, smallz4cat.c:189-205): every frame offset
+//                   classified as a possible size word, the candidates listed, linked and walked by one
+//                   wavefront 64 at a time; k_unlz4_index (one lane walks the size words) is the in-launch
+//                   fallback for what the candidates cannot settle
 //   k_unlz4_sizes   one wavefront per block: token headers only -> decoded length, validation, and
 //                   the block's sequence list (literal run, match length, offset, frame offset of
 //                   the literals), recorded 64 at a time as coalesced 16-byte entries
@@ -20,8 +23,14 @@
 //                   through a ticket (placement independent), each publishes a done flag (agent
 //                   release), a waiter polls relaxed, then acquires; every spin is bounded.
 //
+//   split mode (blocks of >= 256 KiB payload): k_unlz4_spec walks every 8 KiB sub-segment from its first
+//                   byte, k_unlz4_join joins each to the true token chain from an assumed entry, k_unlz4_fix
+//                   checks the assumptions per block (re-joining the wrong ones), k_unlz4_sub decodes every
+//                   sub-segment into a value-or-reference image, k_unlz4_pack resolves the references
+//
 // Byte work only: decoding one block is a chain of sequences (each match may read the bytes the one
-// before it wrote), so the parallelism is one wavefront per block and 64 bytes per copy step.
+// before it wrote), so the parallelism is one wavefront per block (or per sub-segment in split mode) and
+// 64 bytes per copy step.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -109,7 +118,8 @@ __device__ __forceinline__ uint32_t seq_cap(const UnBlock& B) { return B.len / 3
 // sub-segment (below): the walk stops at its first token start >= stop (W.exit) and, with kMark, sets
 // bit (token start - mb) of the LDS mask for every sequence it parsed; with kMerge, it stops before a
 // token start whose bit is set in that LDS mask (W.merged: the speculative walk of the sub-segment
-// parsed from there on already).
+// parsed from there on already).  With kMark, cum (when given) receives each recorded sequence's output
+// offset from r0 (the bytes the sequences before it decode), stored like seq.
 struct WalkEnd {
   uint32_t exit;    // block-relative frame offset where the walk stopped
   uint32_t ns;      // sequences recorded
@@ -119,7 +129,7 @@ struct WalkEnd {
 template <bool kMark, bool kMerge>
 __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane, uint32_t r0,
                                uint32_t stop, uint4* __restrict__ seq, uint32_t cap, uint32_t* maskLds, uint32_t mb,
-                               WalkEnd& W)
+                               WalkEnd& W, uint32_t* __restrict__ cum = nullptr)
 {
   W = WalkEnd{r0, 0u, 0u, 0u};
   if (B.stored) {  // uncompressed block (smallz4cat.c:329-343)
@@ -131,17 +141,23 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
   uint64_t r = B.src + r0, w = 0;  // frame cursor; bytes decoded so far
   uint32_t ns = 0;
   uint4 buf = make_uint4(0u, 0u, 0u, 0u);
-  auto push = [&](uint32_t tok, uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel) {
+  uint32_t bufc = 0;
+  // before: the bytes decoded from r0 up to this sequence
+  auto push = [&](uint32_t tok, uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel, uint32_t before) {
+    const uint32_t l = ns & 63u;
     if constexpr (kMark) {
       if (lane == 0) atomicOr(&maskLds[(tok - mb) >> 5], 1u << ((tok - mb) & 31));
+      bufc = un_wrlane(bufc, before, l);
     }
-    const uint32_t l = ns & 63u;
     buf.x = un_wrlane(buf.x, lits, l);
     buf.y = un_wrlane(buf.y, ml, l);
     buf.z = un_wrlane(buf.z, off, l);
     buf.w = un_wrlane(buf.w, frel, l);
     ns++;
-    if ((ns & 63u) == 0u) seq[ns - 64u + lane] = buf;
+    if ((ns & 63u) == 0u) {
+      seq[ns - 64u + lane] = buf;
+      if (kMark && cum) cum[ns - 64u + lane] = bufc;
+    }
   };
   auto merge_at = [&](uint32_t tok) -> bool {
     if constexpr (kMerge) return (maskLds[(tok - mb) >> 5] >> ((tok - mb) & 31)) & 1u;
@@ -168,7 +184,7 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
     w += lits;
     r += lits;
     if (r == end) {  // the last sequence has literals only
-      push(tokAt, (uint32_t)lits, 0u, 0u, frel);
+      push(tokAt, (uint32_t)lits, 0u, 0u, frel, (uint32_t)(w - lits));
       return 1;
     }
     if (r + 2 > end) return 2;
@@ -184,7 +200,7 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
         ml += x;
       } while (x == 255);
     }
-    push(tokAt, (uint32_t)lits, (uint32_t)ml, off, frel);
+    push(tokAt, (uint32_t)lits, (uint32_t)ml, off, frel, (uint32_t)(w - lits));
     w += ml;
     return 0;
   };
@@ -240,7 +256,7 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
       }
       const uint32_t lits = (pk >> 4) & 15u, nib = pk & 15u;
       const uint32_t ml = kMinMatch + nib + (nib == 15u ? pk >> 24 : 0u);
-      push(rr, lits, ml, off, rr + 1u);
+      push(rr, lits, ml, off, rr + 1u, (uint32_t)w);
       w += lits + ml;
       rr += 3u + lits + (nib == 15u ? 1u : 0u);
     }
@@ -266,7 +282,10 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
   }
   if (ns & 63u) {
     const uint32_t b = ns & ~63u;
-    if (lane < (ns & 63u)) seq[b + lane] = buf;
+    if (lane < (ns & 63u)) {
+      seq[b + lane] = buf;
+      if (kMark && cum) cum[b + lane] = bufc;
+    }
   }
   W.exit = (uint32_t)(r - B.src);
   W.ns = ns;
@@ -274,9 +293,6 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
   return w;
 }
 
-#ifndef SZ4_UNLZ4_VEC
-#define SZ4_UNLZ4_VEC 1  // 0: k_unlz4_sizes walks the token chain one sequence at a time (A/B)
-#endif
 
 // every lane receives the sum of its 16-lane row
 __device__ __forceinline__ uint32_t un_row_sum(uint32_t v)
@@ -574,9 +590,6 @@ __device__ uint64_t unlz4_decode(const uint8_t* __restrict__ f, uint64_t n, cons
   return w;
 }
 
-#ifndef SZ4_UNLZ4_DEC_VEC
-#define SZ4_UNLZ4_DEC_VEC 1  // 0: k_unlz4_blocks replays one sequence at a time (A/B)
-#endif
 
 // inclusive max-scan over the 64 lanes (rows by DPP shifts, then the row broadcasts)
 __device__ __forceinline__ uint32_t un_scan_max(uint32_t v)
@@ -1090,11 +1103,7 @@ __global__ __launch_bounds__(64) void k_unlz4_sizes(const uint8_t* __restrict__ 
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
   WalkEnd W;
-#if SZ4_UNLZ4_VEC
   const uint64_t size = unlz4_walk_vec(f, n, B, lane, seq_base(seqAll, B, bi), seq_cap(B), W);
-#else
-  const uint64_t size = unlz4_walk<false, false>(f, n, B, lane, 0u, B.len, seq_base(seqAll, B, bi), seq_cap(B), nullptr, 0u, W);
-#endif
   if (lane == 0) {
     blk[bi].size = size;
     blk[bi].nseq = W.ns;
@@ -1117,14 +1126,9 @@ __global__ __launch_bounds__(64) void k_unlz4_blocks(const uint8_t* __restrict__
   const uint32_t bi = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
   if (bi >= nb) return;
   const UnBlock B = blk[bi];
-#if SZ4_UNLZ4_DEC_VEC
   __shared__ uint32_t slot[64];
   const uint64_t got = unlz4_decode_vec(f, n, B, bi, lane, seq_base(const_cast<uint4*>(seqAll), B, bi), out, ring, slot,
                                         dict, dl, blk, done, status);
-#else
-  const uint64_t got = unlz4_decode(f, n, B, bi, lane, seq_base(const_cast<uint4*>(seqAll), B, bi), out, ring, dict, dl, blk,
-                                    done, status);
-#endif
   if (lane == 0 && got != B.size) atomicOr(status, 1u);
   // publish: this wave's stores drained, written back (agent release), then the flag
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1144,10 +1148,22 @@ __device__ __forceinline__ uint4* sub_spec(uint4* seq, uint32_t g) { return seq 
 
 // one wavefront per sub-segment: the token chain as if a token started at its first byte, every token
 // start it parsed as a bit.  Wherever the true chain meets one of those starts, the two are the same
-// chain from there on (k_unlz4_fix).
+// chain from there on (k_unlz4_fix).  Side tables for k_unlz4_fix (kUnAuxWords per sub-segment): the
+// mask, its prefix bit counts per word, and every speculative sequence's output offset, so that the
+// rank of a token start and the bytes from it to the sub-segment's end are two loads.
+__device__ __forceinline__ uint32_t* sub_mask(uint32_t* aux, uint32_t g) { return aux + (uint64_t)g * kUnAuxWords; }
+__device__ __forceinline__ uint16_t* sub_mpre(uint32_t* aux, uint32_t g)
+{
+  return reinterpret_cast<uint16_t*>(aux + (uint64_t)g * kUnAuxWords + kSubWords);
+}
+__device__ __forceinline__ uint32_t* sub_cum(uint32_t* aux, uint32_t g)
+{
+  return aux + (uint64_t)g * kUnAuxWords + kSubWords + kSubWords / 2;
+}
+
 __global__ __launch_bounds__(64) void k_unlz4_spec(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
                                                    UnSub* __restrict__ subs, uint32_t nsub, uint4* __restrict__ seq,
-                                                   uint32_t* __restrict__ masks)
+                                                   uint32_t* __restrict__ aux)
 {
   __shared__ uint32_t mask[kSubWords];
   const uint32_t g = blockIdx.x, lane = threadIdx.x;
@@ -1158,24 +1174,146 @@ __global__ __launch_bounds__(64) void k_unlz4_spec(const uint8_t* __restrict__ f
   const UnBlock B = blk[U.block];
   const uint32_t s0 = U.k * kUnSub, s1 = min(s0 + kUnSub, B.len);
   WalkEnd W{s0, 0u, 0u, 0u};
-  const uint64_t sz = B.stored ? 0ull : unlz4_walk<true, false>(f, n, B, lane, s0, s1, sub_spec(seq, g), kUnSubCap, mask, s0, W);
+  const uint64_t sz = B.stored ? 0ull
+                               : unlz4_walk<true, false>(f, n, B, lane, s0, s1, sub_spec(seq, g), kUnSubCap, mask, s0, W,
+                                                         sub_cum(aux, g));
   __syncthreads();
-  for (uint32_t w = lane; w < kSubWords; w += 64) masks[(uint64_t)g * kSubWords + w] = mask[w];
+  // the mask (4 words per lane) and its exclusive prefix bit counts per word
+  static_assert(kSubWords == 256, "four mask words per lane");
+  uint32_t m[4], c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    m[k] = mask[4 * lane + k];
+    c += __popc(m[k]);
+  }
+  uint32_t pre = un_incl_scan_add(c, lane) - c;
+  uint32_t* gm = sub_mask(aux, g);
+  uint16_t* gp = sub_mpre(aux, g);
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    gm[4 * lane + k] = m[k];
+    gp[4 * lane + k] = (uint16_t)pre;
+    pre += __popc(m[k]);
+  }
   if (lane == 0) {
     subs[g].specN = B.stored ? 0u : W.ns;
     subs[g].specExit = B.stored ? s1 : W.exit;
     subs[g].specFlags = B.stored ? 0u : ((sz == kNone ? 1u : 0u) | (W.end ? 2u : 0u));
+    subs[g].specBytes = sz == kNone ? 0u : (uint32_t)sz;
   }
 }
 
-// one wavefront per block: the true chain enters sub-segment k at the exit of sub-segment k - 1; where
-// the speculative walk of k parsed that token start, its list is the true one from there, else the
-// chain is re-parsed from the entry until it meets a speculative start (or leaves the sub-segment).
-// Output: per sub-segment the re-parsed prefix, the first speculative sequence kept, its output offset
-// and length; per block the decoded length (kNone: malformed, as the whole-block walk would find).
+// The join of sub-segment g (block-relative payload [a0, a1)) from an entry t of the true token chain:
+// where the speculative walk of g parsed that token start, its list is the true one from there; else the
+// chain is re-parsed from t until it meets a speculative start (a wrong start falls into the true chain
+// within a few tokens) or leaves the sub-segment.  Output: the re-parsed prefix (preN, in sub_pre), the
+// first speculative sequence kept, the bytes decoded, the exit and whether the block ended.
+struct Join {
+  uint32_t preN, specFrom, outLen, exit;
+  bool ended, ok;
+};
+__device__ Join un_join(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, const UnSub& U, uint32_t g,
+                        uint32_t lane, uint32_t t, bool ended, uint4* __restrict__ seq, uint32_t* __restrict__ aux,
+                        uint32_t* mask)
+{
+  const uint32_t a0 = U.k * kUnSub, a1 = min(a0 + kUnSub, B.len);
+  Join J{0u, U.specN, 0u, t, ended, true};
+  if (B.stored) {  // an uncompressed block: its bytes as they are
+    J.specFrom = 0;
+    J.outLen = a1 - a0;
+    J.exit = a1;
+    J.ended = a1 == B.len;
+    return J;
+  }
+  if (ended || t >= a1) return J;  // nothing of the chain starts here
+  for (uint32_t w = lane; w < kSubWords; w += 64) mask[w] = sub_mask(aux, g)[w];
+  __syncthreads();
+  bool merged = (mask[(t - a0) >> 5] >> ((t - a0) & 31)) & 1u;
+  if (!merged) {
+    WalkEnd W;
+    const uint64_t sz = unlz4_walk<false, true>(f, n, B, lane, t, a1, sub_pre(seq, g), kUnSubCap, mask, a0, W);
+    if (sz == kNone) {
+      J.ok = false;
+    } else {
+      J.preN = W.ns;
+      J.outLen = (uint32_t)sz;
+      merged = W.merged != 0;
+      J.exit = W.exit;
+      J.ended = W.end != 0;
+    }
+  }
+  if (J.ok && merged) {
+    if (U.specFlags & 1u) {  // the true chain runs into the malformed sequence the walk met
+      J.ok = false;
+    } else {
+      const uint32_t x = J.exit - a0;
+      J.specFrom = (uint32_t)sub_mpre(aux, g)[x >> 5] + (uint32_t)__popc(mask[x >> 5] & ((1u << (x & 31)) - 1u));
+      J.outLen += U.specBytes - (J.specFrom < U.specN ? sub_cum(aux, g)[J.specFrom] : U.specBytes);
+      J.exit = U.specExit;
+      J.ended = (U.specFlags & 2u) != 0;
+    }
+  }
+  __syncthreads();
+  return J;
+}
+
+constexpr uint32_t kJoinRounds = 1;
+
+__device__ __forceinline__ void un_store_join(UnSub* __restrict__ subs, uint32_t g, const Join& J, uint32_t entry,
+                                              bool assumedEnded)
+{
+  subs[g].preN = J.preN;
+  subs[g].specFrom = J.specFrom;
+  subs[g].outLen = J.outLen;
+  subs[g].joinEntry = entry;
+  // (read by the next sub-segment's wavefront while a join round runs)
+  __hip_atomic_store(&subs[g].joinExit, J.exit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&subs[g].joinFlags, (assumedEnded ? 1u : 0u) | (J.ok ? 0u : 2u) | (J.ended ? 4u : 0u),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one wavefront per sub-segment: its join from an ASSUMED entry.  Round 0 assumes the true chain enters
+// where the previous sub-segment's speculative walk left (it does whenever the chain met that walk within
+// the previous sub-segment: then it leaves where the walk left -- about 85 % of Silesia's 8 KiB pieces);
+// a later round assumes the exit of the previous sub-segment's latest join, and joins again only where
+// that changed the assumption: after r rounds every sub-segment is right whose chain of wrong guesses is
+// shorter than r.  A round may read the previous sub-segment's record while its own wavefront rewrites it;
+// whatever it reads is only an assumption, which k_unlz4_fix checks against the true chain.
+__global__ __launch_bounds__(64) void k_unlz4_join(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
+                                                   UnSub* __restrict__ subs, uint32_t nsub, uint4* __restrict__ seq,
+                                                   uint32_t* __restrict__ aux, uint32_t round)
+{
+  __shared__ uint32_t mask[kSubWords];
+  const uint32_t g = blockIdx.x, lane = threadIdx.x;
+  if (g >= nsub) return;
+  const UnSub U = subs[g];
+  uint32_t t = 0;
+  bool ended = false;
+  if (U.k != 0) {
+    if (round == 0) {
+      t = subs[g - 1].specExit;
+      ended = (subs[g - 1].specFlags & 2u) != 0;
+    } else {
+      t = __hip_atomic_load(&subs[g - 1].joinExit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ended = (__hip_atomic_load(&subs[g - 1].joinFlags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4u) != 0;
+      if (t == U.joinEntry && ended == ((U.joinFlags & 1u) != 0)) return;  // the same assumption as before
+    }
+  } else if (round != 0) {
+    return;  // the first sub-segment's entry is known
+  }
+  const UnBlock B = blk[U.block];
+  const Join J = un_join(f, n, B, U, g, lane, t, ended, seq, aux, mask);
+  if (lane == 0) un_store_join(subs, g, J, t, ended);
+}
+
+// one wavefront per block: the true chain enters sub-segment k where k - 1's join left.  Sub-segments are
+// taken 64 at a time: lane j's join (k_unlz4_join) holds if its assumed entry is the true one, which by
+// induction is the recorded exit of lane j - 1; up to the first that does not hold, every output offset is
+// one prefix sum; that one is joined again from its true entry, and the next batch starts after it.
+// Per block: the decoded length, or kNone when the block is malformed (as the whole-block walk finds).
 __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f, uint64_t n, UnBlock* __restrict__ blk,
                                                   uint32_t nb, UnSub* __restrict__ subs, uint4* __restrict__ seq,
-                                                  const uint32_t* __restrict__ masks)
+                                                  uint32_t* __restrict__ aux)
 {
   __shared__ uint32_t mask[kSubWords];
   const uint32_t bi = blockIdx.x, lane = threadIdx.x;
@@ -1184,63 +1322,56 @@ __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f,
   if (B.subCount == 0) return;  // an empty block (not split)
   uint32_t t = 0, outRel = 0;
   bool ok = true, ended = false;
-  for (uint32_t k = 0; k < B.subCount; k++) {
-    const uint32_t g = B.subFirst + k;
-    const uint32_t s0 = k * kUnSub, s1 = min(s0 + kUnSub, B.len);
-    const uint32_t specN = subs[g].specN, specExit = subs[g].specExit, specFlags = subs[g].specFlags;
-    uint32_t preN = 0, specFrom = specN, outLen = 0;
-    if (B.stored) {
-      outLen = s1 - s0;  // an uncompressed block: its bytes as they are
-      t = s1;
-      ended = s1 == B.len;
-    } else if (!ended && t < s1) {
-      for (uint32_t w = lane; w < kSubWords; w += 64) mask[w] = masks[(uint64_t)g * kSubWords + w];
-      __syncthreads();
-      bool merged = (mask[(t - s0) >> 5] >> ((t - s0) & 31)) & 1u;
-      if (!merged) {
-        WalkEnd W;
-        const uint64_t sz = unlz4_walk<false, true>(f, n, B, lane, t, s1, sub_pre(seq, g), kUnSubCap, mask, s0, W);
-        if (sz == kNone) {
-          ok = false;
-          break;
-        }
-        preN = W.ns;
-        outLen = (uint32_t)sz;
-        merged = W.merged != 0;
-        t = W.exit;
-        ended = W.end != 0;
-      }
-      if (merged) {
-        if (specFlags & 1u) {  // the true chain runs into the malformed sequence the walk met
-          ok = false;
-          break;
-        }
-        // rank of the entry among the speculative token starts, and the bytes from there on
-        const uint32_t x = t - s0;
-        uint32_t below = 0;
-        for (uint32_t w = lane; w < kSubWords; w += 64) {
-          const uint32_t m = mask[w];
-          below += w * 32 + 32 <= x ? __popc(m) : (w * 32 < x ? __popc(m & ((1u << (x - w * 32)) - 1u)) : 0u);
-        }
-        for (int d = 32; d >= 1; d >>= 1) below += (uint32_t)__shfl_xor((int)below, d, 64);
-        specFrom = below;
-        const uint4* sp = sub_spec(seq, g);
-        uint32_t bytes = 0;
-        for (uint32_t e = specFrom + lane; e < specN; e += 64) bytes += sp[e].x + sp[e].y;
-        for (int d = 32; d >= 1; d >>= 1) bytes += (uint32_t)__shfl_xor((int)bytes, d, 64);
-        outLen += bytes;
-        t = specExit;
-        ended = (specFlags & 2u) != 0;
-      }
-      __syncthreads();
+  uint32_t k = 0;
+  while (k < B.subCount && ok) {
+    const uint32_t kj = k + lane;
+    const bool in = kj < B.subCount;
+    const uint32_t g = B.subFirst + (in ? kj : k);
+    const uint32_t entry = in ? subs[g].joinEntry : 0u, exit = in ? subs[g].joinExit : 0u;
+    const uint32_t flags = in ? subs[g].joinFlags : 2u, outLen = in ? subs[g].outLen : 0u;
+    // the true entry and end state of lane j: lane j - 1's join (lane 0: the batch's)
+    uint32_t tEntry = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 1u) & 63u) << 2), (int)exit);
+    uint32_t pFlags = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 1u) & 63u) << 2), (int)flags);
+    bool tEnded = (pFlags & 4u) != 0;
+    if (lane == 0) {
+      tEntry = t;
+      tEnded = ended;
+    }
+    const bool holds = in && entry == tEntry && ((flags & 1u) != 0) == tEnded;
+    const uint64_t notHeld = ~__ballot(holds);
+    const uint32_t nOk = notHeld ? (uint32_t)__builtin_ctzll(notHeld) : 64u;
+    const uint64_t bad = __ballot(lane < nOk && (flags & 2u));
+    if (bad) {  // a held join met a malformed sequence: the block is malformed
+      ok = false;
+      break;
+    }
+    if (nOk) {
+      const bool mine = lane < nOk;
+      const uint32_t incl = un_incl_scan_add(mine ? outLen : 0u, lane);
+      if (mine) subs[g].outRel = outRel + incl - outLen;
+      outRel += un_rdlane(incl, nOk - 1u);
+      t = un_rdlane(exit, nOk - 1u);
+      ended = (un_rdlane(flags, nOk - 1u) & 4u) != 0;
+      k += nOk;
+      if (nOk == 64u) continue;
+    }
+    if (k >= B.subCount) break;
+    // sub-segment k again, from its true entry
+    const uint32_t gk = B.subFirst + k;
+    const UnSub U = subs[gk];
+    const Join J = un_join(f, n, B, U, gk, lane, t, ended, seq, aux, mask);
+    if (!J.ok) {
+      ok = false;
+      break;
     }
     if (lane == 0) {
-      subs[g].preN = preN;
-      subs[g].specFrom = specFrom;
-      subs[g].outRel = outRel;
-      subs[g].outLen = outLen;
+      un_store_join(subs, gk, J, t, ended);
+      subs[gk].outRel = outRel;
     }
-    outRel += outLen;
+    outRel += J.outLen;
+    t = J.exit;
+    ended = J.ended;
+    k++;
   }
   if (lane == 0) blk[bi].size = ok && ended && t == B.len ? (uint64_t)outRel : kNone;
 }
@@ -1319,38 +1450,45 @@ __global__ __launch_bounds__(64) void k_unlz4_sub(const uint8_t* __restrict__ f,
   }
 }
 
-// pointer jumping: every reference is replaced by what its target holds (a value, or a reference to an
-// earlier byte); *flag is raised while references remain
-__global__ __launch_bounds__(256) void k_unlz4_resolve(uint32_t* __restrict__ img, uint64_t total, uint32_t* __restrict__ flag)
+// image -> bytes, references resolved on the way: a word kUnRef | p is "the same byte as output position
+// p", and p's word is a value or a reference to an earlier byte (each hop lands in an earlier
+// sub-segment), so following it ends.  A resolved word is written back, which shortens the chains other
+// lanes follow through it; a lane may read a word before or after another lane's write-back, and both are
+// the same byte.  hops: the longest chain followed (atomic max).
+__global__ __launch_bounds__(256) void k_unlz4_pack(uint32_t* __restrict__ img, uint64_t total, uint8_t* __restrict__ out,
+                                                    uint32_t* __restrict__ hops)
 {
-  bool left = false;
-  for (uint64_t o = (uint64_t)blockIdx.x * 256 + threadIdx.x; o < total; o += (uint64_t)gridDim.x * 256) {
-    const uint32_t v = img[o];
-    if (v & kUnRef) {
-      const uint32_t w = img[v & ~kUnRef];
-      img[o] = w;
-      left |= (w & kUnRef) != 0;
+  uint32_t most = 0;
+  auto resolve = [&](uint64_t o, uint32_t v) -> uint32_t {
+    if (!(v & kUnRef)) return v;
+    uint32_t h = 0, w = v;
+    while (w & kUnRef) {
+      w = __hip_atomic_load(&img[w & ~kUnRef], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      h++;
     }
-  }
-  if (__ballot(left) && (threadIdx.x & 63) == 0) atomicOr(flag, 1u);
-}
-
-__global__ __launch_bounds__(256) void k_unlz4_pack(const uint32_t* __restrict__ img, uint64_t total, uint8_t* __restrict__ out)
-{
+    __hip_atomic_store(&img[o], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    most = h > most ? h : most;
+    return w;
+  };
   for (uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; o < total; o += (uint64_t)gridDim.x * 1024) {
     if (o + 4 <= total && ((reinterpret_cast<uintptr_t>(out + o) & 3u) == 0)) {
       const uint4 v = *reinterpret_cast<const uint4*>(img + o);
-      *reinterpret_cast<uint32_t*>(out + o) = (v.x & 0xFFu) | ((v.y & 0xFFu) << 8) | ((v.z & 0xFFu) << 16) | (v.w << 24);
+      const uint32_t a = resolve(o, v.x), b = resolve(o + 1, v.y), c = resolve(o + 2, v.z), d = resolve(o + 3, v.w);
+      *reinterpret_cast<uint32_t*>(out + o) = (a & 0xFFu) | ((b & 0xFFu) << 8) | ((c & 0xFFu) << 16) | (d << 24);
     } else {
-      for (uint64_t j = o; j < o + 4 && j < total; j++) out[j] = (uint8_t)img[j];
+      for (uint64_t j = o; j < o + 4 && j < total; j++) out[j] = (uint8_t)resolve(j, img[j]);
     }
   }
+  const uint32_t m = __reduce_max_sync(~0ull, most);
+  if ((threadIdx.x & 63u) == 0 && m) atomicMax(hops, m);
 }
 
 void launch_unlz4_split_sizes(const uint8_t* f, uint64_t n, UnBlock* blk, uint32_t nb, UnSub* subs, uint32_t nsub,
                               uint4* seq, uint32_t* masks, hipStream_t s)
 {
   if (nsub) hipLaunchKernelGGL(k_unlz4_spec, dim3(nsub), dim3(64), 0, s, f, n, blk, subs, nsub, seq, masks);
+  for (uint32_t round = 0; round < kJoinRounds && nsub; round++)
+    hipLaunchKernelGGL(k_unlz4_join, dim3(nsub), dim3(64), 0, s, f, n, blk, subs, nsub, seq, masks, round);
   if (nb) hipLaunchKernelGGL(k_unlz4_fix, dim3(nb), dim3(64), 0, s, f, n, blk, nb, subs, seq, masks);
 }
 
@@ -1360,16 +1498,10 @@ void launch_unlz4_split_decode(const uint8_t* f, uint64_t n, const UnBlock* blk,
   if (nsub) hipLaunchKernelGGL(k_unlz4_sub, dim3(nsub), dim3(64), 0, s, f, n, blk, subs, nsub, seq, image, dict, dl);
 }
 
-void launch_unlz4_resolve(uint32_t* image, uint64_t total, uint32_t* flag, hipStream_t s)
-{
-  const uint64_t g = std::min<uint64_t>((total + 255) / 256, 8192);
-  if (total) hipLaunchKernelGGL(k_unlz4_resolve, dim3((uint32_t)g), dim3(256), 0, s, image, total, flag);
-}
-
-void launch_unlz4_pack(const uint32_t* image, uint64_t total, uint8_t* out, hipStream_t s)
+void launch_unlz4_pack(uint32_t* image, uint64_t total, uint8_t* out, uint32_t* hops, hipStream_t s)
 {
   const uint64_t g = std::min<uint64_t>((total + 1023) / 1024, 8192);
-  if (total) hipLaunchKernelGGL(k_unlz4_pack, dim3((uint32_t)g), dim3(256), 0, s, image, total, out);
+  if (total) hipLaunchKernelGGL(k_unlz4_pack, dim3((uint32_t)g), dim3(256), 0, s, image, total, out, hops);
 }
 
 void launch_unlz4_index(const uint8_t* f, uint64_t n, UnBlock* blk, uint64_t maxBlocks, uint64_t* meta, hipStream_t s)

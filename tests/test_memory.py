@@ -115,6 +115,27 @@ def test_split_decoder_falls_back_to_blockwise_under_limit():
         comp.close()
 
 
+def test_split_decoder_output_counted_under_limit():
+    """a bound between the split plan's own buffers and those plus the output buffer.  The
+    split plan fits, the output does not beside it: the frame is planned again block by block (and the
+    index scratch is released) instead of failing with SZ4_E_NOMEM."""
+    comp = _fresh()
+    try:
+        text = synth.enwik8_like(24 << 20, seed=36)
+        frame = comp.lz4(text)  # 4 MiB dependent blocks: split mode
+        comp.trim()
+        assert comp.unlz4(frame) == text
+        whole = comp.device_bytes()  # frame + split plan + index scratch + output
+        comp.trim()
+        limit = whole - len(text) // 2  # the plan fits, the output beside it does not
+        comp.set_device_limit(limit)
+        assert comp.unlz4(frame) == text
+        assert comp.device_bytes() <= limit
+        comp.set_device_limit(0)
+    finally:
+        comp.close()
+
+
 def test_pool_cap_trims_released_contexts():
     """The drop-in's context pool: a context returned holding more than the cap is trimmed."""
     from smallz4_amd import _native

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Diagnostic: k_find_big's phase clocks and counters from a SZ4_DIAG=6 build of the library
-(tools/build_diag.sh 6 -> smallz4_amd/lib/libsmallz4_amd_diag.so): workgroup-summed shader-clock ticks
+(tools/build_diag.sh 6 -> smallz4_amd/lib/libsmallz4_amd_diag6.so): workgroup-summed shader-clock ticks
 per phase (group discovery, window load, run-group pieces / buckets / search, class path, the prefix
 maximum) on a Silesia-shaped input at 4 MiB blocks, -9."""
 import ctypes
@@ -8,7 +8,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SMALLZ4_AMD_LIB"] = os.path.join(ROOT, "smallz4_amd", "lib", "libsmallz4_amd_diag.so")
+os.environ["SMALLZ4_AMD_LIB"] = os.path.join(ROOT, "smallz4_amd", "lib", "libsmallz4_amd_diag6.so")
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 

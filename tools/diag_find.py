@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Diagnostic (python3 tools/diag_find.py MB [max_chain] [enwik8|zu|silesia]): k_find_sorted's per-wavefront counters from a SZ4_DIAG=3 build of the library
-(smallz4_amd/lib/libsmallz4_amd_diag.so, built by tools/build_diag.sh): below-chunk candidate steps
+(smallz4_amd/lib/libsmallz4_amd_diag3.so, built by tools/build_diag.sh 3): below-chunk candidate steps
 (dB), shift-register steps (dL), improve calls (dBi), extension steps (dLi) and cycles per wave."""
 import ctypes
 import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["SMALLZ4_AMD_LIB"] = os.path.join(ROOT, "smallz4_amd", "lib", "libsmallz4_amd_diag.so")
+os.environ["SMALLZ4_AMD_LIB"] = os.path.join(ROOT, "smallz4_amd", "lib", "libsmallz4_amd_diag3.so")
 sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
