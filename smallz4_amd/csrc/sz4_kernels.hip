@@ -417,6 +417,7 @@ constexpr int kSortThreads = 1024;
 constexpr int kSortWaves = kSortThreads / 64;
 constexpr uint32_t kSortBatch = 8;                          // elements per lane per tile
 constexpr uint32_t kSortTile = kSortThreads * kSortBatch;   // 8192 elements staged per tile
+constexpr uint32_t kCoopBucket = 4096;  // a high-digit bucket larger than this is sorted by the whole workgroup
 
 __device__ __forceinline__ uint32_t pos_bits(uint32_t W) { return W <= 65536u ? 16u : 17u; }
 __device__ __forceinline__ uint32_t key_hash(uint32_t key, uint32_t posBits)
@@ -438,6 +439,7 @@ struct SortLds {
   uint32_t nEx;
   uint32_t bstart[257];            // MSD: first slot of every high-digit bucket
   uint32_t bnext;                  // MSD: the next bucket a wave takes
+  uint32_t nCoop;                  // buckets of more than kCoopBucket elements (step 4)
 };
 
 static_assert(sizeof(SortLds) <= 65536, "k_find_sorted sorts its segment inside the 64 KiB window buffer");
@@ -523,7 +525,10 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
   if (tid == 0) {
     L.bstart[256] = E;
     L.bnext = 0;
+    L.nCoop = 0;
   }
+  __syncthreads();
+  if (tid < 256 && L.bstart[tid + 1] - L.bstart[tid] > kCoopBucket) atomicAdd(&L.nCoop, 1u);
 
   // 2. the stable pass by the high digit (buckets of equal high digit, positions ascending), keys from the
   //    text, a tile at a time ranked and reordered in LDS; every bucket is then sorted by its low digit by
@@ -601,18 +606,42 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
   uint32_t* gs32 = pos32 + E;
   // 3. every high-digit bucket by one wavefront, taken from a counter: its low digits counted, their
   //    exclusive prefix is each hash group's start (no scan over the segment), and the elements (in
-  //    position order) are ranked stably by ballot, 64 at a time, straight to their final slots
+  //    position order) are ranked stably by ballot, 64 at a time, straight to their final slots.
+  //    A bucket of more than kCoopBucket elements (one frequent key: a run of one byte value, zero pages)
+  //    is left to step 4, where the whole workgroup sorts it
+  const uint32_t lowMask = 255u;
+  // element e of the bucket starting at b0 to its slot g + r (g: its hash group's first slot)
+  auto place = [&](uint32_t e, uint32_t g, uint32_t r) {
+    const uint32_t rel = e & posMask;
+    if (small) {
+      pos16[g + r] = (uint16_t)rel;
+      gs16[g + r] = (uint16_t)g;
+    } else {
+      pos32[g + r] = rel;
+      gs32[g + r] = g;
+    }
+  };
+  // the lanes of one 64-element batch with the same low digit as this lane's: (all of them, those below)
+  auto peers_of = [&](bool valid, uint32_t x, uint64_t& below) -> uint64_t {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const uint64_t m = __ballot((x >> b) & 1);
+      peers &= ((x >> b) & 1) ? m : ~m;
+    }
+    below = peers & ((1ull << lane) - 1ull);
+    return peers;
+  };
   {
     uint32_t* run = L.cnt[wave];                 // per low digit: elements placed so far
     uint32_t* pre = L.tile + wave * 512u;        // per low digit: first slot inside the bucket
-    const uint32_t lowMask = 255u;
     while (true) {
       uint32_t d = 0;
       if (lane == 0) d = atomicAdd(&L.bnext, 1u);
       d = rdlane(d, 0);
       if (d >= 256u) break;
       const uint32_t b0 = L.bstart[d], b1 = L.bstart[d + 1];
-      if (b0 == b1) continue;
+      if (b0 == b1 || b1 - b0 > kCoopBucket) continue;
       for (uint32_t x = lane; x < 256u; x += 64) run[x] = 0;
       __builtin_amdgcn_wave_barrier();
       for (uint32_t i = b0 + lane; i < b1; i += 64) atomicAdd(&run[(src[i] >> pb) & lowMask], 1u);
@@ -640,25 +669,9 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
         const bool valid = i < b1;
         const uint32_t e = valid ? src[i] : 0u;
         const uint32_t x = (e >> pb) & lowMask;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-          const uint64_t m = __ballot((x >> b) & 1);
-          peers &= ((x >> b) & 1) ? m : ~m;
-        }
-        const uint64_t below = peers & ((1ull << lane) - 1ull);
-        if (valid) {
-          const uint32_t g = b0 + pre[x];
-          const uint32_t slot = g + run[x] + (uint32_t)__popcll(below);
-          const uint32_t rel = e & posMask;
-          if (small) {
-            pos16[slot] = (uint16_t)rel;
-            gs16[slot] = (uint16_t)g;
-          } else {
-            pos32[slot] = rel;
-            gs32[slot] = g;
-          }
-        }
+        uint64_t below;
+        const uint64_t peers = peers_of(valid, x, below);
+        if (valid) place(e, b0 + pre[x], run[x] + (uint32_t)__popcll(below));
         __builtin_amdgcn_wave_barrier();
         if (valid && below == 0) run[x] += (uint32_t)__popcll(peers);
         __builtin_amdgcn_wave_barrier();
@@ -666,6 +679,44 @@ __device__ __forceinline__ void sort_segment(const uint8_t* __restrict__ in, con
     }
   }
   __syncthreads();
+  // 4. the big buckets, each by the whole workgroup: wave w counts the low digits of the w-th sixteenth
+  //    of it, every (digit, wave) gets its first slot (digit-major, waves in position order: stable), and
+  //    each wave ranks its part by ballot as in step 3
+  for (uint32_t d = 0; d < 256u && L.nCoop; d++) {
+    const uint32_t b0 = L.bstart[d], b1 = L.bstart[d + 1];
+    if (b1 - b0 <= kCoopBucket) continue;  // uniform
+    const uint32_t per = (b1 - b0 + kSortWaves - 1) / kSortWaves;
+    const uint32_t c0 = b0 + wave * per, c1 = min(c0 + per, b1);
+    uint32_t* run = L.cnt[wave];
+    for (uint32_t x = lane; x < 256u; x += 64) run[x] = 0;
+    __syncthreads();
+    for (uint32_t i = c0 + lane; i < c1; i += 64) atomicAdd(&run[(src[i] >> pb) & lowMask], 1u);
+    __syncthreads();
+    if (tid < 256) {  // digit tid: the waves' exclusive offsets inside it, its total
+      uint32_t acc = 0;
+      for (uint32_t w = 0; w < kSortWaves; w++) {
+        const uint32_t c = L.cnt[w][tid];
+        L.cnt[w][tid] = acc;
+        acc += c;
+      }
+      L.tileCnt[tid] = acc;
+    }
+    __syncthreads();
+    digit_scan(tid < 256 ? L.tileCnt[tid] : 0u, L.tileStart, L.wsum);  // every hash group's start
+    for (uint32_t i0 = c0; i0 < c1; i0 += 64) {
+      const uint32_t i = i0 + lane;
+      const bool valid = i < c1;
+      const uint32_t e = valid ? src[i] : 0u;
+      const uint32_t x = (e >> pb) & lowMask;
+      uint64_t below;
+      const uint64_t peers = peers_of(valid, x, below);
+      if (valid) place(e, b0 + L.tileStart[x], run[x] + (uint32_t)__popcll(below));
+      __builtin_amdgcn_wave_barrier();
+      if (valid && below == 0) run[x] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+  }
 }
 
 
