@@ -65,8 +65,10 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
  * Any n in bounded memory: the blocks are compressed in pieces of at most
- * sz4_set_batch_chunk bytes (1.5 GiB by default: about 54-90 GB of scratch; under a
- * sz4_set_device_limit bound the pieces shrink to about 1/64 of it).
+ * sz4_set_batch_chunk bytes (by default 1.5 GiB, capped so that the scratch -- under 50 bytes
+ * per piece byte -- takes at most a quarter of the device memory the context could use now;
+ * under a sz4_set_device_limit bound about 1/64 of the bound).  A piece whose scratch cannot
+ * be allocated is halved and retried, down to 16 MiB, before SZ4_E_NOMEM.
  *
  *   d_in, d_out   device pointers (d_out capacity out_cap bytes)
  *   block_size    1 .. 4 MiB
@@ -121,7 +123,8 @@ int sz4_lz4_stream(sz4_ctx* ctx, sz4_get_bytes get_bytes, sz4_send_bytes send_by
 void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
- * device scratch is about 36-60 bytes per piece byte.  0 restores the 1.5 GiB default. */
+ * device scratch is about 36-50 bytes per piece byte.  An explicit size is not capped by free memory.
+ * 0 restores the default (1.5 GiB, capped by free memory). */
 void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured

@@ -4223,6 +4223,108 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   if (lane == 0) state[idx] = make_uint4(kLazyCap, kLazyCap + m, q | (mode << 31), 0u);
 }
 
+// The join of sub-segment idx to the true walk from entry ex (q | mode << 31): the first speculative search
+// at or after it; if that is the entry in the same mode, the speculative walk is the true one from there,
+// else the walk is redone from the entry until it meets the speculative walk (same position, same mode) or
+// leaves the sub-segment.  The redone searches go to fix[0, f); returns (merged, f, the speculative index it
+// met: m when it did not, the exit); *bad: more than kLazyCap searches (cannot happen).
+struct LazyJoin {
+  uint32_t f, iMerge, exit;
+  bool merged;
+};
+__device__ LazyJoin lazy_join(LazyWalker& w, const uint32_t* spec, uint32_t m, uint32_t* fix, uint32_t ex, uint32_t aNext,
+                              uint32_t specExit, bool& bad)
+{
+  const uint32_t lane = lane_id();
+  const uint32_t entry = ex & 0x7FFFFFFFu, emode = ex >> 31;
+  auto first_at = [&](uint32_t from, uint32_t p) -> uint32_t {
+    for (uint32_t b = from; b < m; b += 64) {
+      const uint64_t ge = __ballot(b + lane < m && spec[b + lane] >= p);
+      if (ge) return b + (uint32_t)__builtin_ctzll(ge);
+    }
+    return m;
+  };
+  auto visited = [&](uint32_t i, uint32_t p, uint32_t md) -> bool { return i < m && spec[i] == p && (i & 1u) == md; };
+  uint32_t i = first_at(0, entry);
+  if (visited(i, entry, emode)) return LazyJoin{0u, i, specExit, true};
+  uint32_t q = entry, md = emode, f = 0;
+  bool merged = false;
+  if (w.wbase == 0xFFFFFFC0u || q < w.wbase || q >= w.wbase + 256) w.start(q);
+  (void)w.next(q, 0);  // q is linked: brings its window in
+  while (q < aNext) {
+    if (f >= kLazyCap) {
+      bad = true;
+      break;
+    }
+    if (lane == 0) fix[f] = q;
+    f++;
+    const uint32_t need = md == 0 ? 0u : w.len(q);
+    md ^= 1u;
+    q = w.next(q + 1, need);
+    if (q >= aNext) break;
+    i = first_at(i, q);
+    if (visited(i, q, md)) {
+      merged = true;
+      break;
+    }
+  }
+  return LazyJoin{f, merged ? i : m, merged ? specExit : (q | (md << 31)), merged};
+}
+
+// every sub-segment k >= 1 joined at once from an ASSUMED entry, sub-segment k - 1's speculative exit (the
+// true one whenever k - 1's true walk met its speculative walk: it then leaves where that one left).  The
+// redone searches go just below the speculative list (slots [kLazyCap - f, kLazyCap), the list itself is
+// kept for k_lazy_fix should the assumption fail); state.x = the join's exit, state.w = 1 << 31 | f << 11 |
+// the speculative index it met (m when none).  k_lazy_fix keeps the joins whose assumption holds.
+__global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_join(const Block* __restrict__ blocks,
+                                                               const uint2* __restrict__ walkSegs, uint32_t nwalk,
+                                                               const Interval* __restrict__ ivAll,
+                                                               const uint32_t* __restrict__ ivCount,
+                                                               const uint32_t* __restrict__ mlen, uint64_t matchBase,
+                                                               uint32_t* __restrict__ slotsAll, uint4* __restrict__ state)
+{
+  __shared__ uint32_t specAll[kWalkWaves][kLazyCap];
+  __shared__ uint32_t fixAll[kWalkWaves][kLazyCap];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * kWalkWaves + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  if (ws.y == 0) return;
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  const uint32_t ex = state[idx - 1].z;
+  const uint4 st = state[idx];
+  const uint32_t a = ws.y * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+  if ((ex & 0x7FFFFFFFu) >= aNext) {
+    if (lane == 0) state[idx].w = 0;  // nothing searched here: k_lazy_fix's own loop (cheap)
+    return;
+  }
+  const uint32_t m = st.y - kLazyCap;
+  uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
+  uint32_t* spec = specAll[wave];
+  uint32_t* fix = fixAll[wave];
+  for (uint32_t t = lane; t < m; t += 64) spec[t] = slots[kLazyCap + t];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  LazyWalker w;
+  w.L = mlen + (B.start - matchBase);
+  w.lastSearch = n - kTailNoMatch;
+  w.iv = ivAll + (uint64_t)ws.x * kMaxIv;
+  w.niv = ivCount[ws.x];
+  w.bstart = B.start;
+  w.wbase = 0xFFFFFFC0u;
+  bool bad = false;
+  const LazyJoin J = lazy_join(w, spec, m, fix, ex, aNext, st.z, bad);
+  __builtin_amdgcn_wave_barrier();
+  for (uint32_t t = lane; t < J.f; t += 64) slots[kLazyCap - J.f + t] = fix[t];
+  if (lane == 0) {
+    state[idx].x = J.exit;
+    state[idx].w = bad ? 0u : (0x80000000u | (J.f << 11) | J.iMerge);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ blocks, const Interval* __restrict__ ivAll,
                                                  const uint32_t* __restrict__ ivCount, const uint32_t* __restrict__ mlen,
                                                  uint64_t matchBase, uint32_t* __restrict__ slotsAll,
@@ -4242,17 +4344,47 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
   w.bstart = B.start;
   w.wbase = 0xFFFFFFC0u;  // no window loaded yet
   uint32_t ex = state[B.walkFirst].z;  // exact exit of sub-segment 0 (walked from the block start)
-  uint4 st = state[B.walkFirst + 1];
-  for (uint32_t k = 1; k < B.walkCount; k++) {
-    const uint32_t idx = B.walkFirst + k;
-    const uint4 stNext = k + 1 < B.walkCount ? state[idx + 1] : make_uint4(0, 0, 0, 0);  // one ahead
+  uint32_t prevSpec = ex;               // the speculative exit of the sub-segment before k (k_lazy_join's assumption)
+  for (uint32_t k = 1; k < B.walkCount;) {
+    {
+      // sub-segments k .. k + 63: lane j's join (k_lazy_join) holds when its assumed entry -- the speculative
+      // exit of k + j - 1 -- is the true one: for j = 0 when it is ex, for j > 0 when lane j - 1's holds and
+      // its join met its speculative walk (then it left where that walk left).  Up to the first that does not
+      // hold, all at once: the redone searches moved in front of the speculative index the join met
+      const uint32_t kj = k + lane;
+      const bool in = kj < B.walkCount;
+      const uint4 sj = in ? state[B.walkFirst + kj] : make_uint4(0u, 0u, 0u, 0u);
+      const uint32_t pExit = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 1u) & 63u) << 2), (int)sj.x);
+      const uint32_t pSpec = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((lane - 1u) & 63u) << 2), (int)sj.z);
+      const bool holds = in && (sj.w >> 31) && (lane == 0 ? ex == prevSpec : pExit == pSpec);
+      const uint64_t notHeld = ~__ballot(holds);
+      const uint32_t nOk = notHeld ? (uint32_t)__builtin_ctzll(notHeld) : 64u;
+      if (lane < nOk) {
+        const uint32_t f = (sj.w >> 11) & 0x7FFu, iM = sj.w & 0x7FFu;
+        const uint32_t start = kLazyCap + iM - f;
+        uint32_t* sl = slotsAll + (uint64_t)(B.walkFirst + kj) * (2 * kLazyCap);
+        if (iM) for (uint32_t t = f; t-- > 0;) sl[start + t] = sl[kLazyCap - f + t];  // (a few; moves up: descending)
+        state[B.walkFirst + kj] = make_uint4(start, sj.y, sj.x, 0u);
+      }
+      if (nOk) {
+        ex = rdlane(sj.x, nOk - 1u);
+        prevSpec = rdlane(sj.z, nOk - 1u);
+        k += nOk;
+        if (nOk == 64u) continue;
+      }
+      if (k >= B.walkCount) break;
+    }
+    // sub-segment k on its own, from its true entry
+    const uint32_t kc = k++;
+    const uint32_t idx = B.walkFirst + kc;
+    const uint4 st = state[idx];
+    prevSpec = st.z;
     const uint32_t entry = ex & 0x7FFFFFFFu, emode = ex >> 31;
-    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+    const uint32_t a = kc * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
     uint32_t* slots = slotsAll + (uint64_t)idx * (2 * kLazyCap);
     const uint32_t m = st.y - kLazyCap;
     if (entry >= aNext) {
       if (lane == 0) state[idx] = make_uint4(st.y, st.y, ex, 0u);  // nothing searched here
-      st = stNext;
       continue;  // ex unchanged: the entry of the next sub-segment
     }
     for (uint32_t t = lane; t < m; t += 64) spec[t] = slots[kLazyCap + t];
@@ -4271,7 +4403,6 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
     if (visited(i, entry, emode)) {
       if (lane == 0) state[idx] = make_uint4(kLazyCap + i, st.y, st.z, 0u);
       ex = st.z;
-      st = stNext;
       __syncthreads();
       continue;
     }
@@ -4303,7 +4434,6 @@ __global__ __launch_bounds__(64) void k_lazy_fix(const Block* __restrict__ block
     for (uint32_t t = lane; t < f; t += 64) slots[start + t] = fix[t];
     ex = merged ? st.z : (q | (md << 31));
     if (lane == 0) state[idx] = make_uint4(start, st.y, ex, 0u);
-    st = stNext;
     __syncthreads();
   }
 }
@@ -6070,6 +6200,8 @@ void launch_lazy(const uint8_t* in, const Block* blocks, uint32_t nblocks, const
   if (!nblocks || !nwalk) return;
   const uint32_t grid = (nwalk + kWalkWaves - 1) / kWalkWaves;
   hipLaunchKernelGGL(k_lazy_walk, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, iv, ivCount, mlen,
+                     matchBase, slots, state);
+  hipLaunchKernelGGL(k_lazy_join, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, iv, ivCount, mlen,
                      matchBase, slots, state);
   hipLaunchKernelGGL(k_lazy_fix, dim3(nblocks), dim3(64), 0, s, blocks, iv, ivCount, mlen, matchBase, slots, state, status);
   hipLaunchKernelGGL(k_lazy_clear, dim3(grid), dim3(64 * kWalkWaves), 0, s, blocks, walkSegs, nwalk, iv, ivCount, mlen,
