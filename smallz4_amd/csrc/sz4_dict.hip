@@ -367,8 +367,13 @@ __global__ __launch_bounds__(256) void k_dict_pe(const uint8_t* __restrict__ in,
 
 // findLongestMatch (smallz4.h:173-255) of every linked position (previousExact set) of every block,
 // over snapshot reads of the exact chains: strictly longer replaces, maxChain counts replacements.
-// Every other position gets (0, 0): not searched.  Grid (positions, blocks).
-// (8 waves per SIMD: the chain walks are latency-bound; 65 VGPRs / 100 SGPRs admitted 6)
+// Every other position gets (0, 0): not searched.  Grid (position ranges, blocks).
+// The chains' lengths are skewed (text: 76 hops on average, 1350 at the 99th percentile), so a wavefront
+// takes kDictSearchPer * 64 consecutive positions as a queue: a lane takes the next one whenever its
+// walk ends, one hop per loop turn, and the wavefront runs for about the mean, not 64 maxima.
+// (8 waves per SIMD: the chain walks are latency-bound)
+constexpr uint32_t kDictSearchPer = 8;
+constexpr uint32_t kDictSearchSpan = 64 * kDictSearchPer;  // positions per wavefront
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_num_sgpr(80))) void k_dict_search(const uint8_t* __restrict__ in, DictPlan P, uint32_t maxChain,
                                                      const uint16_t* __restrict__ pe, const uint16_t* __restrict__ prevX0,
                                                      uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
@@ -376,88 +381,131 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
 {
   const uint32_t b = blockIdx.y;
   const Block B = P.blocks[b];
-  const uint64_t size = B.end - B.start;
-  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i >= size) return;
-  const uint64_t pos = B.start + i;
-  if (maxChain > (uint32_t)kGreedyMax && i + kTailLiterals >= size) sel[pos] = 0;
-  uint32_t bestLen = 0, bestDist = 0;
-  if (P.ivCount[b] && P.skipped(b, pos)) {
-    // same-letter shortcut (smallz4.h:636-641): the interval's distance-1 match, one byte shorter per step
-    const Interval* v = P.iv + (uint64_t)b * kMaxIv;
-    uint32_t k = 0;
-    while (!(pos >= v[k].lo && pos < v[k].hi)) k++;
-    bestLen = (uint32_t)(v[k].La - (pos - v[k].a));
-    bestDist = 1;
-  } else if (i + kTailNoMatch <= size && pe[pos] != 0) {
-    const int64_t back = P.back(b);
-    const uint64_t stop = B.end - kTailLiterals;
-    bestLen = 1;
-    uint32_t steps = maxChain;
-    uint32_t hop = read_slot(P, pe, prevX0, (uint32_t)(pos & kWindow), b, (int64_t)i, B.start, back);
-    uint64_t backDist = 0;
-    const int64_t room = (int64_t)(stop - pos);
-    while (hop != 0) {
-      backDist += hop;
-      if (backDist > kWindow) break;
-      hop = read_slot(P, pe, prevX0, (uint32_t)((pos - backDist) & kWindow), b, (int64_t)i, B.start, back);
-      const int64_t need = (int64_t)bestLen + 1;
-      if (need > room) break;
-      uint64_t c = pos - backDist;
-      if (hop == 1u && bestLen >= 4u) {
-        // In a run of one byte value v every inserted position's exact predecessor is the one before it,
-        // so the chain steps down the run one position at a time.  Once p holds a match of bestLen and
-        // its byte at bestLen is not v, a candidate c' of the run with c' + need <= run end fails the
-        // first word of phase 1 (bytes need-4 .. need-1: p's differ from v at bestLen, c''s are all v):
-        // the whole stretch is rejected, and the walk continues at its bottom c_j with the hop read there.
-        // Stretch: read at y gives 1 for y in (c_j, c] when y - 1 and y - 2 are inserted positions of
-        // the run's interior (first + 1 .. end - 4) of this block (no shortcut interval among them).
-        const uint64_t rk = (c - P.runBase) >> 6;
-        const uint2 rt = c >= P.runBase && rk < P.runChunks ? P.runTab[rk] : make_uint2(0u, 0u);
-        if (rt.y != 0u && c + (uint64_t)need <= rt.y && c + 3 <= rt.y && in[pos + bestLen] != in[c]) {
-          uint64_t cj = max((uint64_t)rt.x + 2, B.start + 2);
-          const uint32_t niv = P.ivCount[b];
+  const uint32_t size = (uint32_t)(B.end - B.start);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t first = (blockIdx.x * 4u + (threadIdx.x >> 6)) * kDictSearchSpan;
+  if (first >= size) return;
+  const uint32_t last = first + kDictSearchSpan < size ? first + kDictSearchSpan : size;
+  const int64_t back = P.back(b);
+  const uint64_t stop = B.end - kTailLiterals;
+  const bool hasIv = P.ivCount[b] != 0;
+  uint32_t cursor = first;  // the wavefront's next untaken position (uniform)
+  uint32_t i = 0, bestLen = 0, bestDist = 0, steps = 0, hop = 0;
+  uint64_t pos = 0, backDist = 0;
+  int64_t room = 0;
+  bool walking = false, live = false, rmq = false;
+  while (true) {
+    // lanes without a position take the next ones, in lane order
+    const uint64_t want = __ballot(!walking);
+    if (want) {
+      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+      if (!walking) {
+        i = cursor + rank;
+        live = i < last;
+      }
+      cursor += (uint32_t)__builtin_popcountll(want);
+      if (!walking && live) {
+        pos = B.start + i;
+        if (maxChain > (uint32_t)kGreedyMax && i + kTailLiterals >= size) sel[pos] = 0;
+        bestLen = 0;
+        bestDist = 0;
+        if (hasIv && P.skipped(b, pos)) {
+          // same-letter shortcut (smallz4.h:636-641): the interval's distance-1 match, one byte shorter per step
           const Interval* v = P.iv + (uint64_t)b * kMaxIv;
-          bool inside = false;
-          for (uint32_t k = 0; k < niv; k++) {
-            if (c >= v[k].lo && c < v[k].hi) inside = true;
-            if (v[k].hi <= c && v[k].hi + 2 > cj) cj = v[k].hi + 2;
+          uint32_t k = 0;
+          while (!(pos >= v[k].lo && pos < v[k].hi)) k++;
+          bestLen = (uint32_t)(v[k].La - (pos - v[k].a));
+          bestDist = 1;
+        } else if (i + kTailNoMatch <= size && pe[pos] != 0) {
+          bestLen = 1;
+          steps = maxChain;
+          hop = read_slot(P, pe, prevX0, (uint32_t)(pos & kWindow), b, (int64_t)i, B.start, back);
+          backDist = 0;
+          room = (int64_t)(stop - pos);
+          walking = true;
+        }
+        if (!walking) {
+          mlen[pos] = bestLen;
+          mdist[pos] = (uint16_t)bestDist;
+          rmq |= bestLen >= kRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
+        }
+      }
+    }
+    if (!__ballot(walking)) {
+      if (cursor >= last) break;
+      continue;
+    }
+    if (walking) {
+      // one candidate of the walk
+      bool done = hop == 0;
+      if (!done) {
+        backDist += hop;
+        done = backDist > kWindow;
+      }
+      if (!done) {
+        hop = read_slot(P, pe, prevX0, (uint32_t)((pos - backDist) & kWindow), b, (int64_t)i, B.start, back);
+        const int64_t need = (int64_t)bestLen + 1;
+        done = need > room;
+        if (!done) {
+          uint64_t c = pos - backDist;
+          if (hop == 1u && bestLen >= 4u) {
+            // In a run of one byte value v every inserted position's exact predecessor is the one before it,
+            // so the chain steps down the run one position at a time.  Once p holds a match of bestLen and
+            // its byte at bestLen is not v, a candidate c' of the run with c' + need <= run end fails the
+            // first word of phase 1 (bytes need-4 .. need-1: p's differ from v at bestLen, c''s are all v):
+            // the whole stretch is rejected, and the walk continues at its bottom c_j with the hop read there.
+            // Stretch: read at y gives 1 for y in (c_j, c] when y - 1 and y - 2 are inserted positions of
+            // the run's interior (first + 1 .. end - 4) of this block (no shortcut interval among them).
+            const uint64_t rk = (c - P.runBase) >> 6;
+            const uint2 rt = c >= P.runBase && rk < P.runChunks ? P.runTab[rk] : make_uint2(0u, 0u);
+            if (rt.y != 0u && c + (uint64_t)need <= rt.y && c + 3 <= rt.y && in[pos + bestLen] != in[c]) {
+              uint64_t cj = max((uint64_t)rt.x + 2, B.start + 2);
+              const uint32_t niv = P.ivCount[b];
+              const Interval* v = P.iv + (uint64_t)b * kMaxIv;
+              bool inside = false;
+              for (uint32_t k = 0; k < niv; k++) {
+                if (c >= v[k].lo && c < v[k].hi) inside = true;
+                if (v[k].hi <= c && v[k].hi + 2 > cj) cj = v[k].hi + 2;
+              }
+              if (!inside && cj < c && pos - cj <= kWindow) {
+                c = cj;
+                backDist = pos - cj;
+                hop = read_slot(P, pe, prevX0, (uint32_t)(cj & kWindow), b, (int64_t)i, B.start, back);
+              }
+            }
           }
-          if (!inside && cj < c && pos - cj <= kWindow) {
-            c = cj;
-            backDist = pos - cj;
-            hop = read_slot(P, pe, prevX0, (uint32_t)(cj & kWindow), b, (int64_t)i, B.start, back);
+          // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
+          int64_t lo = need - 4;
+          while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
+          if (lo <= 0) {
+            // phase 2: forward from the first new byte; 32 bytes per step while they all agree (the loads of
+            // a step are independent: one latency per 32 bytes in a long run instead of one per 4)
+            int64_t hi = need;
+            while (hi + 32 <= room) {
+              uint32_t x = 0;
+#pragma unroll
+              for (int k = 0; k < 32; k += 4) x |= gload4(in, pos + hi + k) ^ gload4(in, c + hi + k);
+              if (x) break;
+              hi += 32;
+            }
+            while (hi + 4 <= room && gload4(in, pos + hi) == gload4(in, c + hi)) hi += 4;
+            while (hi < room && in[pos + hi] == in[c + hi]) hi++;
+            bestLen = (uint32_t)hi;
+            bestDist = (uint32_t)backDist;
+            done = --steps == 0;
           }
         }
       }
-      // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
-      int64_t lo = need - 4;
-      while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
-      if (lo > 0) continue;
-      // phase 2: forward from the first new byte; 32 bytes per step while they all agree (the loads of
-      // a step are independent: one latency per 32 bytes in a long run instead of one per 4)
-      int64_t hi = need;
-      while (hi + 32 <= room) {
-        uint32_t x = 0;
-#pragma unroll
-        for (int k = 0; k < 32; k += 4) x |= gload4(in, pos + hi + k) ^ gload4(in, c + hi + k);
-        if (x) break;
-        hi += 32;
+      if (done) {
+        mlen[pos] = bestLen;
+        mdist[pos] = (uint16_t)bestDist;
+        rmq |= bestLen >= kRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
+        walking = false;
       }
-      while (hi + 4 <= room && gload4(in, pos + hi) == gload4(in, c + hi)) hi += 4;
-      while (hi < room && in[pos + hi] == in[c + hi]) hi++;
-      bestLen = (uint32_t)hi;
-      bestDist = (uint32_t)backDist;
-      if (--steps == 0) break;
     }
   }
-  mlen[pos] = bestLen;
-  mdist[pos] = (uint16_t)bestDist;
   // optimal levels search every linked position: the parse's range-minimum flag is set here
-  if (maxChain > (uint32_t)kLazyMax) {
-    const bool rmq = bestLen >= kRmqLen && !(bestDist == 1u && bestLen >= kSameLetter);
-    if (__ballot(rmq) && lane_id() == 0) atomicOr(longFlag + b, kFlagRmq);
-  }
+  if (maxChain > (uint32_t)kLazyMax && __ballot(rmq) && lane == 0) atomicOr(longFlag + b, kFlagRmq);
 }
 
 // Greedy/lazy levels: the skip bookkeeping (smallz4.h:726-744) over the linked positions of a block
@@ -840,7 +888,7 @@ int launch_dict_parallel(const DictArgs& A, hipStream_t s)
   }
   if (maxOwn)
     hipLaunchKernelGGL(k_dict_pe, dim3((maxOwn + 255) / 256, nb), dim3(256), 0, s, A.in, P, A.ph, A.prevH, A.pe);
-  hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 255) / 256, nb), dim3(256), 0, s, A.in, P, A.maxChain, A.pe, A.prevX,
+  hipLaunchKernelGGL(k_dict_search, dim3((maxSize + 4 * kDictSearchSpan - 1) / (4 * kDictSearchSpan), nb), dim3(256), 0, s, A.in, P, A.maxChain, A.pe, A.prevX,
                      A.mlen, A.mdist, A.sel, A.longFlag);
   if (A.maxChain <= (uint32_t)kLazyMax && A.nwalk) {
     hipLaunchKernelGGL(k_dict_lz_walk, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
