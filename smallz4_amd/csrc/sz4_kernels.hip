@@ -885,7 +885,9 @@ __device__ __forceinline__ uint32_t prefix_run(const Src& src, uint64_t p, uint6
 // improvement, step limit).  Prefixes are capped at kLongCap: a target reaching it keeps the marker
 // kLongMatch and is finished by k_find (pass 2), which walks long repeats in text order.
 // ================================================================================================
-constexpr uint32_t kLongCap = 32;    // bounded chains: prefixes >= this are finished by pass 2
+// bounded chains: prefixes >= this are finished by pass 2 (32 sent 4x more targets to k_find's second chain walk:
+// -3/-6/-8 on configs[1] 10191/7742/9444 -> 11347/8925/11334 MB/s at 256, frames identical)
+constexpr uint32_t kLongCap = 256;
 constexpr uint32_t kLongCap9 = 256;  // -9: pass 1 extends exactly up to this
 constexpr uint32_t kSatQ = 128;  // saturated-candidate queue per wavefront (flushed at 64)
 // broadcast chunk list: >= slots / 64 + number of groups of >= 64 slots (64 Ki slots with the LDS
@@ -1085,6 +1087,9 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       SZ4_D3(dBi++;)
       const uint32_t x1 = k1 ^ me1, x2 = k2 ^ me2;
       uint32_t kk = x1 ? 4u + ((uint32_t)__builtin_ctz(x1) >> 3) : x2 ? 8u + ((uint32_t)__builtin_ctz(x2) >> 3) : 12u;
+      // 12 bytes equal and bestLen >= 12: it improves only if bytes bestLen - 3 .. bestLen match too (one
+      // 4-byte test before the extension; inside a same-letter run every candidate passes the 12-byte mask)
+      if (kk == 12u && bestLen >= 12u && src.ld4(p + bestLen - 3) != src.ld4(cpos + bestLen - 3)) kk = 0;
       if (kk == 12u) {
         bool open = true;
         while (open && kk < limit) {

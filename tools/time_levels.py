@@ -4,6 +4,7 @@ smallz4.cpp:232-238: -N -> N for N <= 8, -9 -> 65535) with the stage split; run 
 `rocprofv3 --kernel-trace --stats` for the per-kernel picture.
     python3 tools/time_levels.py 3 6 [--mb 100]"""
 import argparse
+import hashlib
 import os
 import sys
 import time
@@ -39,7 +40,9 @@ def main():
             size = comp.compress_blocks_device(t_in.data_ptr(), n, out.data_ptr(), cap, 65536, chain)
         dt = (time.perf_counter() - t0) / a.reps
         st = {k: round(v, 3) for k, v in comp.last_stage_ms().items()}
-        print(f"-{lv}: {n / dt / 1e6:.1f} MB/s ({dt * 1e3:.3f} ms), ratio {size / n:.4f}, stages {st}", flush=True)
+        sha = hashlib.sha256(out[:size].cpu().numpy().tobytes()).hexdigest()[:16]
+        print(f"-{lv}: {n / dt / 1e6:.1f} MB/s ({dt * 1e3:.3f} ms), ratio {size / n:.4f}, frame {sha}, stages {st}",
+              flush=True)
 
 
 if __name__ == "__main__":
