@@ -65,7 +65,7 @@ uint64_t sz4_bound(uint64_t n, uint32_t block_size);
  * (4-byte size word + payload) are exactly what smallz4::lz4 emits for that
  * block compressed on its own (reference smallz4.h:476-813 with one block).
  * Any n in bounded memory: the blocks are compressed in pieces of at most
- * sz4_set_batch_chunk bytes (by default 1.5 GiB, capped so that the scratch -- under 50 bytes
+ * sz4_set_batch_chunk bytes (by default 448 MiB, split into equal pieces, and capped so that the scratch -- under 50 bytes
  * per piece byte -- takes at most a quarter of the device memory the context could use now;
  * under a sz4_set_device_limit bound about 1/64 of the bound).  A piece whose scratch cannot
  * be allocated is halved and retried, down to 16 MiB, before SZ4_E_NOMEM.
@@ -124,7 +124,7 @@ void sz4_set_stream_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Input bytes per internal piece of sz4_compress_blocks_device (whole blocks, at least one); the
  * device scratch is about 36-50 bytes per piece byte.  An explicit size is not capped by free memory.
- * 0 restores the default (1.5 GiB, capped by free memory). */
+ * 0 restores the default (448 MiB, capped by free memory). */
 void sz4_set_batch_chunk(sz4_ctx* ctx, uint64_t bytes);
 
 /* Device time (milliseconds) of each pipeline stage of the last call, measured

@@ -144,7 +144,7 @@ class Compressor:
         self._lib.sz4_set_stream_chunk(self._h, int(nbytes))
 
     def set_batch_chunk(self, nbytes: int):
-        """Input bytes per internal piece of compress_blocks(_device) (whole blocks; 0 = default 1.5 GiB)."""
+        """Input bytes per internal piece of compress_blocks(_device) (whole blocks; 0 = default 448 MiB)."""
         self._lib.sz4_set_batch_chunk(self._h, int(nbytes))
 
     # -- data-parallel entry point --------------------------------------------------------------

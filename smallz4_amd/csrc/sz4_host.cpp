@@ -32,11 +32,11 @@ namespace {
 
 constexpr uint64_t kPad = 64;                 // bytes of slack after every staged input
 constexpr uint64_t kSegTargets = 65536;       // target positions per segment
-// batch API pieces: 1.5 GiB of input (54-90 GB of scratch, sized for the MI355X's 288 GB): a rank's
-// 1.25 GiB slice of configs[4] is ONE piece (the per-block repair wavefronts of its 5120 blocks run
-// together: one latency-bound walk instead of one per piece), and a piece of 256 KiB blocks holds four
-// or more repair wavefronts per SIMD
-constexpr uint64_t kBatchChunkDefault = 3ull << 29;
+// batch API pieces: at most 448 MiB of input, split evenly (a rank's 1.25 GiB slice of configs[4]: three
+// pieces of 427 MiB), so that the scratch (48.6 B per piece byte at 256 KiB blocks) stays under ~21 GiB.
+// Round 5's 1.5 GiB pieces took ~61 GiB for +14 % on configs[4]: the slice in ONE piece runs the per-block
+// parse repair wavefronts of its 5120 blocks together, one latency-bound launch instead of one per piece
+constexpr uint64_t kBatchChunkDefault = 448ull << 20;
 constexpr uint64_t kScratchPerByte = 50;     // device scratch per piece byte, upper bound (36-49 measured)
 constexpr uint64_t kPieceFloor = 16ull << 20;  // smallest batch piece the out-of-memory retry goes down to
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
@@ -1477,7 +1477,10 @@ int sz4_compress_blocks_device(sz4_ctx* c, const void* d_in, uint64_t n, uint32_
     else
       (void)hipGetLastError();
   }
-  uint64_t piece = std::max<uint64_t>(block_size, chunk / block_size * block_size);
+  // equal pieces (the last one is not a small remainder): ceil(n / chunk) of them, whole blocks each
+  const uint64_t nPieces = (n + chunk - 1) / std::max<uint64_t>(chunk, 1);
+  const uint64_t even = (n + nPieces - 1) / nPieces;
+  uint64_t piece = std::max<uint64_t>(block_size, (even + block_size - 1) / block_size * block_size);
   float stageSum[kStages] = {};
   uint64_t pos = 0;
   c->hostBytes.clear();

@@ -5104,6 +5104,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
   SZ4_D7(
   // k_dp_fix<false> per block: serial positions, closed-form chunks, literal chunks, segments walked
   uint64_t d7Serial = 0, d7Closed = 0, d7Lit = 0, d7Segs = 0;
+  uint64_t d7Tk[4] = {0, 0, 0, 0};  // ticks in literal / closed / serial chunks, and in the rmq stores
   const uint64_t d7t0 = __builtin_readcyclecounter();
   )
   if constexpr (kPar) {
@@ -5309,6 +5310,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
       }
       closedRun = false;
       SZ4_D7(if (h == hi) d7Segs++;)
+      SZ4_D7(const uint64_t d7c0 = __builtin_readcyclecounter(); const uint64_t d7l0 = d7Lit, d7k0 = d7Closed;)
       if (noMatch || __ballot(in && cL >= (uint32_t)kMinMatch) == 0) {
         SZ4_D7(d7Lit++;)
         // no match anywhere in the chunk: all literals, costs in closed form (lane t = position h - t)
@@ -5423,7 +5425,14 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
         if (Lk >= (uint32_t)kMinMatch) {
           if (Lk >= kSameLetter && Dk == 1) {
             best = Lk;
-            minCost = cost_at(i, i + (int32_t)Lk) + 4 + (Lk - 19) / 255;
+            // positions of one run share its end: one (dependent, uncached) load per run, as in the
+            // closed-form chunks
+            const int32_t E = i + (int32_t)Lk;
+            if (E != runE) {
+              runC = cost_at(i, E);
+              runE = E;
+            }
+            minCost = runC + 4 + (Lk - 19) / 255;
           } else {
             auto cost_j = [&](int32_t j) -> uint32_t { return cost_at(i, j); };
             const int32_t Ei = i + (int32_t)Lk;  // <= top + 1
@@ -5478,6 +5487,8 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
           }
         }
       }
+      SZ4_D7(const uint64_t d7c1 = __builtin_readcyclecounter();
+             d7Tk[d7Lit != d7l0 ? 0 : d7Closed != d7k0 ? 1 : 2] += d7c1 - d7c0;)
       if (rmq) {
         if (!done) {
           // UP of the chunk, DOWN of a finished rmq block
@@ -5509,6 +5520,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
           if (!kPar && lane == 0) convBlk[k] = (uint32_t)jb;  // (k_dp_fix<true> has no tables)
         }
       }
+      SZ4_D7(d7Tk[3] += __builtin_readcyclecounter() - d7c1;)
     }
     if constexpr (kPar) {
       const int32_t rd = wave_max_i32(readTop > maxReach ? readTop : maxReach);
@@ -5543,6 +5555,7 @@ const Block* __restrict__ blocks, const DpSeg* __restrict__ dpSegs,
     atomicMax((unsigned long long*)&sz4_diag[6], (unsigned long long)dt);
     atomicAdd((unsigned long long*)&sz4_diag[7], 1ull);
     if (rmq) atomicAdd((unsigned long long*)&sz4_diag[8], 1ull);
+    for (int q = 0; q < 4; q++) atomicAdd((unsigned long long*)&sz4_diag[9 + q], (unsigned long long)d7Tk[q]);
   }
   )
 }

@@ -34,6 +34,9 @@ def main():
     print(f"  blocks {nb} (rmq {int(d[8])}), segments walked {int(d[3])}, serial positions {int(d[0])} "
           f"(max per block {int(d[4])}), closed chunks {int(d[1])}, literal chunks {int(d[2])}")
     print(f"  ticks per block: mean {int(d[5]) / max(nb, 1):.4g}, max {int(d[6])}")
+    tk = [int(x) for x in d[9:13]]
+    print("  ticks by chunk kind (sum over blocks): " + ", ".join(
+        f"{k} {v:.4g} ({100 * v / max(int(d[5]), 1):.1f} %)" for k, v in zip(("literal", "closed", "serial", "rmq stores"), tk)))
 
 
 if __name__ == "__main__":
