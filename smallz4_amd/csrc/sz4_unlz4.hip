@@ -1381,7 +1381,9 @@ __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f,
 // wavefront writes it).  A sub-segment's own earlier bytes are copied as they are (values or
 // references): recent ones through an LDS ring of the last kRingU words, older ones from the image after
 // the wave drained its stores, as in unlz4_decode.
-constexpr uint32_t kRingU = 4096;
+// 8 KiB of LDS per one-wave workgroup: 20 per CU (5 waves per SIMD; 4096 words held it to 2.5, and the
+// latency-bound copy loop needs the waves: Silesia at 4 MiB blocks 16.4 -> 14.9 ms, profiles/r06/r06aa)
+constexpr uint32_t kRingU = 2048;
 constexpr uint32_t kSyncU = kRingU / 2;
 
 __global__ __launch_bounds__(64) void k_unlz4_sub(const uint8_t* __restrict__ f, uint64_t n, const UnBlock* __restrict__ blk,
