@@ -14,7 +14,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 if [ -z "${SKIP_BENCH:-}" ]; then
-  timeout -k 10 400 python3 "$R/bench.py" $EXTRA > "$OUT/bench.json" 2> "$OUT/bench.err"
+  timeout -k 10 700 python3 "$R/bench.py" $EXTRA > "$OUT/bench.json" 2> "$OUT/bench.err"
 fi
 cd /tmp
 ARGS="--steps 10 --warmup 3 --no-verify --no-stream --no-dict --no-shapes --no-levels --cpu-seconds 0.5 $EXTRA"

@@ -73,7 +73,10 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
         total = (10 << 30)
         lo, hi = shard.shard_range(total, bs, 0, world)
         data = synth.zeros_urandom_range(lo, hi, seed=10)
+    # a rank's process runs only its batch calls: what earlier tests left in the shared session context
+    # (decoder, stream and dictionary buffers) is released first
     before = compressor.device_bytes()
+    compressor.trim()
     part = compressor.compress_blocks(data, bs, 65535, header="none")
     footprint = compressor.device_bytes()  # before the decoder's own scratch joins it
     spans = _spans(part)
@@ -100,7 +103,7 @@ def test_rank0_slice_full_size(compressor, workload, world, bs):
     print(f"{workload} rank-0 slice {len(data)} B: context holds {footprint / 2**30:.2f} GiB "
           f"({footprint / len(data):.1f} B per input byte; {before / 2**30:.2f} GiB before)")
     # bounded: sz4_compress_blocks_device runs equal pieces of at most 448 MiB (36-49 B of scratch per piece
-    # byte, plus what earlier tests left in the shared context), whatever the slice's length
+    # byte), whatever the slice's length
     assert footprint < 24 << 30
 
 
