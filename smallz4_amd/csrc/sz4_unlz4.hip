@@ -39,6 +39,16 @@
 #include "sz4_internal.h"
 
 namespace sz4 {
+#ifndef SZ4_DIAG
+#define SZ4_DIAG 0
+#endif
+#if SZ4_DIAG == 8
+// diagnostic build 8: k_unlz4_fix's serial re-joins (tools/diag_unlz4.py)
+__device__ uint64_t sz4_udiag[16];
+#define SZ4_D8(...) __VA_ARGS__
+#else
+#define SZ4_D8(...)
+#endif
 
 namespace {
 
@@ -217,6 +227,14 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
     // byte << 24, or ~0 when the header needs the byte-wise path (literal run >= 15, a second match
     // extension byte, or bytes past the register window).  The walk costs one readlane per sequence.
     win.fill(r, lane);
+    // kMerge: the mask words this window can reach, one per lane (a token start's merge bit by readlane, not
+    // one dependent LDS read per sequence); the mask is read-only while a join walks
+    uint32_t mw = 0, mw0 = 0;
+    if constexpr (kMerge) {
+      mw0 = (uint32_t)(r - B.src - mb) >> 5;
+      const uint32_t wi = mw0 + lane;
+      mw = lane < 8u && wi < kUnSub / 32u ? maskLds[wi] : 0u;
+    }
     uint32_t cand[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -235,7 +253,8 @@ __device__ uint64_t unlz4_walk(const uint8_t* __restrict__ f, uint64_t n, const 
     uint32_t rr = (uint32_t)(r - B.src);
     bool slow = false, stopped = false;
     while (rr < fastEnd) {
-      if (kMerge && rr != (uint32_t)(r - B.src) && merge_at(rr)) {
+      if (kMerge && rr != (uint32_t)(r - B.src) &&
+          ((un_rdlane(mw, ((rr - mb) >> 5) - mw0) >> ((rr - mb) & 31u)) & 1u)) {
         stopped = true;
         break;
       }
@@ -447,6 +466,226 @@ __device__ uint64_t unlz4_walk_vec(const uint8_t* __restrict__ f, uint64_t n, co
     r = B.src + rr;
     if (rr < fastEnd && !slow) continue;  // refill
     if (r >= end) break;
+    if (ns >= cap) {
+      W.exit = rr;
+      return kNone;
+    }
+    const int e = one_seq();
+    if (e == 2) {
+      W.exit = (uint32_t)(r - B.src);
+      return kNone;
+    }
+    if (e == 1) break;
+  }
+  W.exit = (uint32_t)(r - B.src);
+  W.ns = ns;
+  W.end = r >= end ? 1u : 0u;
+  return w;
+}
+
+// unlz4_walk<kMark, kMerge> of a sub-segment on the vector unit, as unlz4_walk_vec: the path through 64
+// window positions at a time by binary lifting.  kMerge (a join): its first token start at or past stop or
+// with its bit set in the read-only LDS mask ends the walk there (W.merged).  kMark (the speculative walk):
+// the path's token starts are OR-ed into the mask 64 window positions at a time (one ballot), and cum
+// receives each sequence's output offset from r0.  Whatever the pre-decoded headers do not cover goes
+// byte-wise, as in unlz4_walk, so the two agree on every frame.
+template <bool kMark, bool kMerge>
+__device__ uint64_t unlz4_walk_v(const uint8_t* __restrict__ f, uint64_t n, const UnBlock& B, uint32_t lane,
+                                 uint32_t r0, uint32_t stop, uint4* __restrict__ seq, uint32_t cap, uint32_t* maskLds,
+                                 uint32_t mb, WalkEnd& W, uint32_t* __restrict__ cum = nullptr)
+{
+  W = WalkEnd{r0, 0u, 0u, 0u};
+  if (B.stored) {
+    W.exit = B.len;
+    W.end = 1;
+    return B.len;
+  }
+  const uint64_t end = B.src + B.len;
+  uint64_t r = B.src + r0, w = 0;
+  uint32_t ns = 0;
+  auto push = [&](uint32_t tokAt, uint32_t lits, uint32_t ml, uint32_t off, uint32_t frel, uint32_t before) {
+    if (lane == 0) {
+      seq[ns] = make_uint4(lits, ml, off, frel);
+      if constexpr (kMark) {
+        atomicOr(&maskLds[(tokAt - mb) >> 5], 1u << ((tokAt - mb) & 31));
+        if (cum) cum[ns] = before;
+      }
+    }
+    ns++;
+  };
+  auto merge_at = [&](uint32_t tok) -> bool {
+    if constexpr (kMerge) return (maskLds[(tok - mb) >> 5] >> ((tok - mb) & 31)) & 1u;
+    return false;
+  };
+  Window win{f, n, 0, 0};
+  auto one_seq = [&]() -> int {
+    const uint32_t tokAt = (uint32_t)(r - B.src);
+    const uint32_t tok = win.byte(r++, lane);
+    uint64_t lits = tok >> 4;
+    if (lits == 15) {
+      uint32_t x;
+      do {
+        if (r >= end) return 2;
+        x = win.byte(r++, lane);
+        lits += x;
+      } while (x == 255);
+    }
+    if (r + lits > end) return 2;
+    const uint32_t frel = (uint32_t)(r - B.src);
+    w += lits;
+    r += lits;
+    if (r == end) {  // the last sequence has literals only
+      push(tokAt, (uint32_t)lits, 0u, 0u, frel, (uint32_t)(w - lits));
+      return 1;
+    }
+    if (r + 2 > end) return 2;
+    const uint32_t off = win.byte(r, lane) | (win.byte(r + 1, lane) << 8);
+    r += 2;
+    if (off == 0) return 2;  // "invalid offset" (smallz4cat.c:265-267)
+    uint64_t ml = kMinMatch + (tok & 15);
+    if (ml == kMinMatch + 15) {
+      uint32_t x;
+      do {
+        if (r >= end) return 2;
+        x = win.byte(r++, lane);
+        ml += x;
+      } while (x == 255);
+    }
+    push(tokAt, (uint32_t)lits, (uint32_t)ml, off, frel, (uint32_t)(w - lits));
+    w += ml;
+    return 0;
+  };
+  const uint32_t fastEnd = min(B.len > 20u ? B.len - 20u : 0u, stop);
+  bool done = false;
+  while (r < end && (uint32_t)(r - B.src) < stop) {
+    if (kMerge && merge_at((uint32_t)(r - B.src))) {
+      W.merged = 1;
+      break;
+    }
+    win.fill(r, lane);
+    uint32_t cand[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t tok = (win.w >> (8 * k)) & 0xFFu;
+      const uint32_t a = 4u * lane + (uint32_t)k + 1u + (tok >> 4);  // window index of the offset
+      const uint32_t ia = (a >> 2) << 2;
+      const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute((int)ia, (int)win.w);
+      const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(ia + 4u), (int)win.w);
+      const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (a & 3u)));
+      const bool ext = (tok & 15u) == 15u;
+      const uint32_t last = a + 1u + (ext ? 1u : 0u);  // last window byte the header reads
+      const bool ok = (tok >> 4) != 15u && last < 256u && !(ext && ((v >> 16) & 0xFFu) == 255u) && (v & 0xFFFFu) != 0u;
+      cand[k] = ok ? (tok | (v << 8)) : 0xFFFFFFFFu;  // v's bytes 0-2: offset, extension byte
+    }
+    const uint32_t wb = (uint32_t)(win.base - B.src);  // window base, block-relative
+    uint32_t rr = (uint32_t)(r - B.src);
+    bool slow = false, bad = false;
+    while (rr < fastEnd) {
+      const uint32_t q0 = rr - wb;
+      if (q0 >= 192u) break;  // refill
+      const uint32_t sb = q0 & ~63u, e = q0 & 63u;
+      const int src = (int)(((sb >> 2) + (lane >> 2)) << 2);
+      const uint32_t g0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[0]);
+      const uint32_t g1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[1]);
+      const uint32_t g2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[2]);
+      const uint32_t g3 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)cand[3]);
+      const uint32_t c = (lane & 2u) ? ((lane & 1u) ? g3 : g2) : ((lane & 1u) ? g1 : g0);
+      const uint32_t pos = wb + sb + lane;  // block-relative frame offset of this lane's token
+      const bool ok = c != 0xFFFFFFFFu && pos < fastEnd;
+      const uint32_t lits = (c >> 4) & 15u, nib = c & 15u;
+      const uint32_t step = 3u + lits + (nib == 15u ? 1u : 0u);
+      uint32_t F[6];
+      F[0] = ok && lane + step < 64u ? lane + step : 64u;
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(F[k - 1] << 2), (int)F[k - 1]);
+        F[k] = F[k - 1] >= 64u ? 64u : g;
+      }
+      uint32_t x = e;
+      {
+        const uint32_t y = un_rdlane(F[5], e);
+        x = y <= lane ? y : x;
+      }
+#pragma unroll
+      for (int k = 4; k >= 0; k--) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(x << 2), (int)F[k]);
+        x = y <= lane ? y : x;
+      }
+      // the path's token starts in this sub-window (its last one may need the byte-wise path); the first of
+      // them at or past stop, or with its merge bit set, ends the walk (positions >= stop are not ok, so
+      // such a token is the path's last)
+      const bool onPath = x == lane && lane >= e;
+      const uint32_t mrel = pos - mb;
+      const bool mbit = kMerge && pos < stop && mrel < kUnSub && ((maskLds[mrel >> 5] >> (mrel & 31u)) & 1u);
+      const uint64_t term = __ballot(onPath && (pos >= stop || mbit));
+      const uint32_t T = term ? (uint32_t)__builtin_ctzll(term) : 64u;
+      const bool tok = onPath && ok && lane < T;
+      const uint64_t tb = __ballot(tok);
+      const uint32_t cnt = (uint32_t)__builtin_popcountll(tb);
+      if (ns + cnt > cap) {  // cannot happen in a well-formed block
+        bad = true;
+        break;
+      }
+      const uint32_t ml = kMinMatch + nib + (nib == 15u ? c >> 24 : 0u);
+      const uint32_t dec = tok ? lits + ml : 0u;
+      uint32_t incl = 0;
+      if constexpr (kMark) incl = un_incl_scan_add(dec, lane);
+      if (tok) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(tb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)tb, 0u));
+        seq[ns + rank] = make_uint4(lits, ml, (c >> 8) & 0xFFFFu, pos + 1u);
+        if (kMark && cum) cum[ns + rank] = (uint32_t)w + incl - dec;
+      }
+      if constexpr (kMark) {
+        // the recorded token starts' bits: 64 consecutive positions from wb + sb (those below mb are none)
+        if (tb && lane == 0) {
+          int32_t m0 = (int32_t)(wb + sb) - (int32_t)mb;
+          uint64_t bits = tb;
+          if (m0 < 0) {
+            bits >>= (uint32_t)(-m0);
+            m0 = 0;
+          }
+          const uint32_t j0 = (uint32_t)m0 >> 5, sh = (uint32_t)m0 & 31u;
+          const uint32_t b0 = (uint32_t)(bits << sh), b1 = (uint32_t)(bits >> (32u - sh));
+          const uint32_t b2 = sh ? (uint32_t)(bits >> (64u - sh)) : 0u;
+          if (b0) atomicOr(&maskLds[j0], b0);
+          if (b1) atomicOr(&maskLds[j0 + 1u], b1);
+          if (b2) atomicOr(&maskLds[j0 + 2u], b2);
+        }
+      }
+      ns += cnt;
+      if constexpr (kMark) {
+        w += un_rdlane(incl, 63);
+      } else {
+        const uint32_t rs = un_row_sum(dec);
+        w += (uint64_t)(un_rdlane(rs, 0) + un_rdlane(rs, 16) + un_rdlane(rs, 32) + un_rdlane(rs, 48));
+      }
+      if (term) {
+        rr = wb + sb + T;
+        W.merged = rr < stop ? 1u : 0u;
+        done = true;
+        break;
+      }
+      const uint32_t p = un_rdlane(x, 63);  // the last token start of the path in this sub-window
+      if (!((__ballot(ok) >> p) & 1ull)) {
+        // a header the window did not pre-decode: from a refilled window, or byte-wise at the window start
+        rr = wb + sb + p;
+        slow = sb + p < 64u;
+        break;
+      }
+      rr = wb + sb + p + un_rdlane(step, p);
+    }
+    if (bad) {
+      W.exit = rr;
+      return kNone;
+    }
+    r = B.src + rr;
+    if (done) break;
+    if (rr < fastEnd && !slow) continue;  // refill
+    if (r >= end || rr >= stop) break;
+    if (kMerge && merge_at(rr)) {
+      W.merged = 1;
+      break;
+    }
     if (ns >= cap) {
       W.exit = rr;
       return kNone;
@@ -1175,8 +1414,8 @@ __global__ __launch_bounds__(64) void k_unlz4_spec(const uint8_t* __restrict__ f
   const uint32_t s0 = U.k * kUnSub, s1 = min(s0 + kUnSub, B.len);
   WalkEnd W{s0, 0u, 0u, 0u};
   const uint64_t sz = B.stored ? 0ull
-                               : unlz4_walk<true, false>(f, n, B, lane, s0, s1, sub_spec(seq, g), kUnSubCap, mask, s0, W,
-                                                         sub_cum(aux, g));
+                               : unlz4_walk_v<true, false>(f, n, B, lane, s0, s1, sub_spec(seq, g), kUnSubCap, mask, s0,
+                                                           W, sub_cum(aux, g));
   __syncthreads();
   // the mask (4 words per lane) and its exclusive prefix bit counts per word
   static_assert(kSubWords == 256, "four mask words per lane");
@@ -1231,7 +1470,7 @@ __device__ Join un_join(const uint8_t* __restrict__ f, uint64_t n, const UnBlock
   bool merged = (mask[(t - a0) >> 5] >> ((t - a0) & 31)) & 1u;
   if (!merged) {
     WalkEnd W;
-    const uint64_t sz = unlz4_walk<false, true>(f, n, B, lane, t, a1, sub_pre(seq, g), kUnSubCap, mask, a0, W);
+    const uint64_t sz = unlz4_walk_v<false, true>(f, n, B, lane, t, a1, sub_pre(seq, g), kUnSubCap, mask, a0, W);
     if (sz == kNone) {
       J.ok = false;
     } else {
@@ -1323,7 +1562,9 @@ __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f,
   uint32_t t = 0, outRel = 0;
   bool ok = true, ended = false;
   uint32_t k = 0;
+  SZ4_D8(const uint64_t d8t0 = __builtin_readcyclecounter(); uint64_t d8Re = 0, d8Quick = 0, d8Tok = 0, d8Tk = 0, d8Merged = 0, d8Batch = 0;)
   while (k < B.subCount && ok) {
+    SZ4_D8(d8Batch++;)
     const uint32_t kj = k + lane;
     const bool in = kj < B.subCount;
     const uint32_t g = B.subFirst + (in ? kj : k);
@@ -1359,7 +1600,10 @@ __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f,
     // sub-segment k again, from its true entry
     const uint32_t gk = B.subFirst + k;
     const UnSub U = subs[gk];
+    SZ4_D8(const uint64_t d8c0 = __builtin_readcyclecounter(); d8Re++;
+           if (ended || t >= min(U.k * kUnSub + kUnSub, B.len)) d8Quick++;)
     const Join J = un_join(f, n, B, U, gk, lane, t, ended, seq, aux, mask);
+    SZ4_D8(d8Tk += __builtin_readcyclecounter() - d8c0; d8Tok += J.preN; if (J.exit == U.specExit) d8Merged++;)
     if (!J.ok) {
       ok = false;
       break;
@@ -1374,6 +1618,20 @@ __global__ __launch_bounds__(64) void k_unlz4_fix(const uint8_t* __restrict__ f,
     k++;
   }
   if (lane == 0) blk[bi].size = ok && ended && t == B.len ? (uint64_t)outRel : kNone;
+  SZ4_D8(if (lane == 0) {
+    const uint64_t dt = __builtin_readcyclecounter() - d8t0;
+    atomicAdd((unsigned long long*)&sz4_udiag[0], 1ull);
+    atomicAdd((unsigned long long*)&sz4_udiag[1], (unsigned long long)B.subCount);
+    atomicAdd((unsigned long long*)&sz4_udiag[2], (unsigned long long)d8Batch);
+    atomicAdd((unsigned long long*)&sz4_udiag[3], (unsigned long long)d8Re);
+    atomicAdd((unsigned long long*)&sz4_udiag[4], (unsigned long long)d8Quick);
+    atomicAdd((unsigned long long*)&sz4_udiag[5], (unsigned long long)d8Tok);
+    atomicAdd((unsigned long long*)&sz4_udiag[6], (unsigned long long)d8Merged);
+    atomicAdd((unsigned long long*)&sz4_udiag[7], (unsigned long long)d8Tk);
+    atomicAdd((unsigned long long*)&sz4_udiag[8], (unsigned long long)dt);
+    atomicMax((unsigned long long*)&sz4_udiag[9], (unsigned long long)dt);
+    atomicMax((unsigned long long*)&sz4_udiag[10], (unsigned long long)d8Re);
+  })
 }
 
 // The decode image: one u32 per output byte, the byte's value (< 256) or kUnRef | p: "the same byte as
@@ -1568,3 +1826,15 @@ void launch_unlz4_blocks(const uint8_t* f, uint64_t n, const UnBlock* blk, uint3
 }
 
 }  // namespace sz4
+#if SZ4_DIAG == 8
+extern "C" int sz4_udiag_read(uint64_t* out, uint64_t n)
+{
+  if (n > 16) n = 16;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(sz4::sz4_udiag), n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int sz4_udiag_clear()
+{
+  uint64_t z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(sz4::sz4_udiag), z, sizeof z, 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+#endif
