@@ -4211,19 +4211,80 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_walk(const Block* __re
   w.niv = ivCount[ws.x];
   w.bstart = B.start;
   w.start(a);
-  uint32_t pos = a, need = 0, mode = 0, m = 0, q;  // mode 0: fresh, 1: lazy
+  // Fresh searches alternate with lazy ones: fresh q -> lazy q2 = the next linked position -> fresh = the
+  // next linked position after skipping len(q2) more.  So the fresh positions form a functional graph, and
+  // inside one 64-position window the walk's fresh positions are found at once (as k_walk does): every
+  // linked lane computes its successor from the window's linked ranks (64 when it leaves the window), F2 ..
+  // F32 by doubling, binary lifting from the entry.  The last fresh position of the window (its successor
+  // elsewhere) and everything across windows go one step at a time through LazyWalker.
+  uint32_t mode = 0, m = 0;  // mode 0: fresh, 1: lazy
+  uint32_t q = w.next(a, 0);
   while (true) {
-    q = w.next(pos, need);
-    if (q >= aNext) break;
-    if (m >= kLazyCap) {  // cannot happen (see kLazyCap); stop rather than overrun
+    if (q >= aNext) break;  // fresh, mode 0
+    if (q >= w.wbase && q < w.wbase + 64) {
+      const uint64_t M = __ballot(w.wL >= (uint32_t)kMinMatch && w.wbase + lane <= w.lastSearch) & ~w.wIv;
+      const uint32_t pc = (uint32_t)__popcll(M);
+      const bool lk = (M >> lane) & 1ull;
+      const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(M >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)M, 0u));
+      // lane k: the lane of the k-th linked position of the window (k < pc)
+      const uint32_t sel = (uint32_t)__builtin_amdgcn_ds_permute((int)((lk ? rk : 63u) << 2), (int)lane);
+      // a fresh search at this lane: its lazy search is the next linked lane, which skips its length more
+      const uint32_t r2 = rk + 1u;
+      const uint32_t l2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r2 < pc ? r2 : 0u) << 2), (int)sel);
+      const uint32_t len2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(l2 << 2), (int)w.wL);
+      const uint32_t r3 = r2 + 1u + len2;
+      const uint32_t l3 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((r3 < pc ? r3 : 0u) << 2), (int)sel);
+      const bool in = lk && r2 < pc && r3 < pc;
+      uint32_t F[6];
+      F[0] = in ? l3 : 64u;
+#pragma unroll
+      for (int k = 1; k < 6; k++) {
+        const uint32_t g = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((F[k - 1] & 63u) << 2), (int)F[k - 1]);
+        F[k] = F[k - 1] >= 64u ? 64u : g;
+      }
+      const uint32_t e = q - w.wbase;
+      uint32_t x = e;
+      {
+        const uint32_t y = rdlane(F[5], e);
+        x = y <= lane ? y : x;
+      }
+#pragma unroll
+      for (int k = 4; k >= 0; k--) {
+        const uint32_t y = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((x & 63u) << 2), (int)F[k]);
+        x = y <= lane ? y : x;
+      }
+      const uint32_t pLast = rdlane(x, 63);  // the window's last fresh position of the walk
+      const bool rec = x == lane && lane >= e && lane != pLast;  // fresh positions with both searches inside
+      const uint64_t rb = __ballot(rec);
+      const uint32_t cnt = (uint32_t)__popcll(rb);
+      if (m + 2u * cnt + 2u > kLazyCap) {  // cannot happen (see kLazyCap); stop rather than overrun
+        q = kLazyEnd;
+        break;
+      }
+      if (rec) {
+        const uint32_t j = m + 2u * __builtin_amdgcn_mbcnt_hi((uint32_t)(rb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)rb, 0u));
+        slots[j] = w.wbase + lane;
+        slots[j + 1u] = w.wbase + l2;
+      }
+      m += 2u * cnt;
+      q = w.wbase + pLast;
+    }
+    // the fresh search at q, its lazy one, the next fresh one -- one step at a time
+    if (m + 2u > kLazyCap) {
       q = kLazyEnd;
       break;
     }
     if (lane == 0) slots[m] = q;
     m++;
-    need = mode == 0 ? 0u : w.len(q);
-    mode ^= 1u;
-    pos = q + 1;
+    const uint32_t q2 = w.next(q + 1, 0);
+    if (q2 >= aNext) {
+      q = q2;
+      mode = 1;
+      break;
+    }
+    if (lane == 0) slots[m] = q2;
+    m++;
+    q = w.next(q2 + 1, w.len(q2));
   }
   if (lane == 0) state[idx] = make_uint4(kLazyCap, kLazyCap + m, q | (mode << 31), 0u);
 }
