@@ -522,6 +522,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
 // it reaches a position the speculative walk searched fresh, and k_dict_lz_clear clears the linked
 // positions nobody searched.  Masks: kWalkSeg bits each, [fresh | kept] per sub-segment.
 constexpr uint32_t kLzWords = kWalkSeg / 32;
+// per sub-segment: [fresh | kept | the join's re-walked positions] bit masks, then the join's record (4 words)
+constexpr uint32_t kLzStride = 3 * kLzWords + 4;
 constexpr uint32_t kLzEnd = 0x7FFFFFFFu;
 
 // the need-th (0-based) linked position at or after pos over a register window of 64 positions
@@ -630,9 +632,77 @@ __global__ __launch_bounds__(64 * 4) void k_dict_lz_walk(const Block* __restrict
     q = lz_step(w, q, md, carry);
   }
   __builtin_amdgcn_wave_barrier();
-  uint32_t* out = masks + (uint64_t)idx * (2 * kLzWords);
+  uint32_t* out = masks + (uint64_t)idx * kLzStride;
   for (uint32_t t = lane; t < 2 * kLzWords; t += 64) out[t] = fresh[t];
   if (lane == 0) state[idx] = make_uint4(q, md, carry, 0u);
+}
+
+// every sub-segment k >= 1 joined at once from an ASSUMED entry, sub-segment k - 1's speculative exit (the
+// true one whenever k - 1's true walk reached a position its speculative walk searched fresh): re-walked
+// from there until it reaches such a position of its own walk (merged) or leaves the sub-segment.  The
+// re-walked positions go to the third mask, the record (exit q, mode, carry, 1 | merged << 1 | from << 2)
+// after it; k_dict_lz_fix keeps the joins whose assumption holds.
+__global__ __launch_bounds__(64 * 4) void k_dict_lz_join(const Block* __restrict__ blocks, const uint2* __restrict__ walkSegs,
+                                                         uint32_t nwalk, const uint32_t* __restrict__ mlen,
+                                                         const uint16_t* __restrict__ pe, uint32_t* __restrict__ masks,
+                                                         const uint4* __restrict__ state)
+{
+  __shared__ uint32_t bits[4][2 * kLzWords];
+  const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const uint32_t idx = blockIdx.x * 4 + wave;
+  if (idx >= nwalk) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint2 ws = walkSegs[idx];
+  if (ws.y == 0) return;
+  const Block B = blocks[ws.x];
+  const uint32_t n = (uint32_t)(B.end - B.start);
+  if (n < (uint32_t)kTailNoMatch) return;
+  uint32_t* m = masks + (uint64_t)idx * kLzStride;
+  const uint4 ex = state[idx - 1];
+  const uint32_t a = ws.y * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+  uint32_t q = ex.x, md = ex.y, carry = ex.z;
+  if (q >= aNext) {  // nothing searched here: k_dict_lz_fix's own loop (cheap)
+    if (lane == 0) m[3 * kLzWords + 3] = 0u;
+    return;
+  }
+  uint32_t* fresh = bits[wave];
+  uint32_t* rep = fresh + kLzWords;
+  for (uint32_t t = lane; t < kLzWords; t += 64) {
+    fresh[t] = m[t];
+    rep[t] = 0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  auto is_fresh = [&](uint32_t p) { return (fresh[(p - a) >> 5] >> ((p - a) & 31)) & 1u; };
+  bool merged = md == 0u && is_fresh(q);
+  if (!merged) {
+    DictWalker w;
+    w.L = mlen + B.start;
+    w.E = pe + B.start;
+    w.last = n - kTailNoMatch;
+    w.start(q);
+    (void)w.next(q, 0u);
+    while (q < aNext) {
+      if (md == 0u && is_fresh(q)) {
+        merged = true;
+        break;
+      }
+      lz_setbit(rep, q - a);
+      q = lz_step(w, q, md, carry);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  for (uint32_t t = lane; t < kLzWords; t += 64) m[2 * kLzWords + t] = rep[t];
+  const uint32_t from = merged ? q - a : kWalkSeg;
+  if (lane == 0) {
+    const uint4 sp = state[idx];
+    const uint4 rec = merged ? make_uint4(sp.x, sp.y, sp.z, 1u | 2u | (from << 2)) : make_uint4(q, md, carry, 1u | (from << 2));
+    m[3 * kLzWords + 0] = rec.x;
+    m[3 * kLzWords + 1] = rec.y;
+    m[3 * kLzWords + 2] = rec.z;
+    m[3 * kLzWords + 3] = rec.w;
+  }
 }
 
 __global__ __launch_bounds__(64) void k_dict_lz_fix(const Block* __restrict__ blocks, const uint32_t* __restrict__ mlen,
@@ -650,11 +720,50 @@ __global__ __launch_bounds__(64) void k_dict_lz_fix(const Block* __restrict__ bl
   w.last = n - kTailNoMatch;
   w.wbase = 0xFFFFFFC0u;  // no window loaded yet
   uint4 ex = state[B.walkFirst];  // sub-segment 0 was walked from the block start: exact
-  for (uint32_t k = 1; k < B.walkCount; k++) {
-    const uint32_t idx = B.walkFirst + k;
+  uint4 prevSpec = ex;            // the speculative exit of the sub-segment before k (k_dict_lz_join's assumption)
+  auto same = [](const uint4& x, const uint4& y) { return x.x == y.x && x.y == y.y && x.z == y.z; };
+  for (uint32_t k = 1; k < B.walkCount;) {
+    {
+      // sub-segments k .. k + 63: lane j's join holds when its assumed entry (the speculative exit of
+      // k + j - 1) is the true one: for j = 0 when it is ex, for j > 0 when lane j - 1's holds and its
+      // join's exit is its speculative exit.  Up to the first that does not hold, all at once
+      const uint32_t kj = k + lane;
+      const bool in = kj < B.walkCount;
+      const uint32_t idxj = B.walkFirst + (in ? kj : k);
+      uint32_t* mj = masks + (uint64_t)idxj * kLzStride;
+      const uint4 sj = state[idxj];
+      const uint4 jr = in ? make_uint4(mj[3 * kLzWords], mj[3 * kLzWords + 1], mj[3 * kLzWords + 2], mj[3 * kLzWords + 3])
+                          : make_uint4(0u, 0u, 0u, 0u);
+      // this lane's join exit equals its speculative exit (then the next sub-segment's assumption holds)
+      const bool exitIsSpec = (jr.w & 2u) != 0u;
+      const bool prevOk = (__ballot(exitIsSpec) << 1 >> lane) & 1ull;  // lane j - 1's
+      const bool holds = in && (jr.w & 1u) && (lane == 0 ? same(ex, prevSpec) : prevOk);
+      const uint64_t notHeld = ~__ballot(holds);
+      const uint32_t nOk = notHeld ? (uint32_t)__builtin_ctzll(notHeld) : 64u;
+      for (uint32_t j = 0; j < nOk; j++) {
+        // kept = the re-walked positions, then the speculative ones from the merge point on
+        uint32_t* mm = masks + (uint64_t)(B.walkFirst + k + j) * kLzStride;
+        const uint32_t from = rdlane(jr.w, j) >> 2;
+        for (uint32_t t = lane; t < kLzWords; t += 64) {
+          const uint32_t lo = t * 32;
+          const uint32_t keepSpec = from <= lo ? 0xFFFFFFFFu : (from >= lo + 32 ? 0u : ~0u << (from - lo));
+          mm[kLzWords + t] = mm[2 * kLzWords + t] | (mm[kLzWords + t] & keepSpec);
+        }
+      }
+      if (nOk) {
+        ex = make_uint4(rdlane(jr.x, nOk - 1u), rdlane(jr.y, nOk - 1u), rdlane(jr.z, nOk - 1u), 0u);
+        prevSpec = make_uint4(rdlane(sj.x, nOk - 1u), rdlane(sj.y, nOk - 1u), rdlane(sj.z, nOk - 1u), 0u);
+        k += nOk;
+        if (nOk == 64u) continue;
+      }
+      if (k >= B.walkCount) break;
+    }
+    const uint32_t kc = k++;
+    const uint32_t idx = B.walkFirst + kc;
     const uint4 spec = state[idx];
-    const uint32_t a = k * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
-    uint32_t* m = masks + (uint64_t)idx * (2 * kLzWords);
+    prevSpec = spec;
+    const uint32_t a = kc * kWalkSeg, aNext = a + kWalkSeg < n ? a + kWalkSeg : n;
+    uint32_t* m = masks + (uint64_t)idx * kLzStride;
     uint32_t q = ex.x, md = ex.y, carry = ex.z;
     if (q >= aNext) {  // nothing searched in this sub-segment
       for (uint32_t t = lane; t < kLzWords; t += 64) m[kLzWords + t] = 0;
@@ -711,7 +820,7 @@ __global__ __launch_bounds__(64 * 4) void k_dict_lz_clear(const Block* __restric
   const uint32_t last = n - kTailNoMatch;
   const uint32_t a = ws.y * kWalkSeg;
   const uint32_t hi = a + kWalkSeg - 1 < last ? a + kWalkSeg - 1 : last;  // inclusive
-  const uint32_t* kept = masks + (uint64_t)idx * (2 * kLzWords) + kLzWords;
+  const uint32_t* kept = masks + (uint64_t)idx * kLzStride + kLzWords;
   bool rmq = false;
   for (uint32_t x0 = a; x0 <= hi; x0 += 64) {
     const uint32_t x = x0 + lane;
@@ -837,7 +946,7 @@ __global__ __launch_bounds__(64) void k_dict_sc(const Block* __restrict__ blocks
   }
 }
 
-uint64_t dict_lz_mask_bytes_per_walk() { return 2 * kLzWords * 4; }
+uint64_t dict_lz_mask_bytes_per_walk() { return kLzStride * 4; }
 
 uint64_t dict_sort_keys_max() { return kBlockMaxLegacy + 64; }
 
@@ -892,6 +1001,8 @@ int launch_dict_parallel(const DictArgs& A, hipStream_t s)
                      A.mlen, A.mdist, A.sel, A.longFlag);
   if (A.maxChain <= (uint32_t)kLazyMax && A.nwalk) {
     hipLaunchKernelGGL(k_dict_lz_walk, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
+                       A.pe, A.lzMasks, A.lzState);
+    hipLaunchKernelGGL(k_dict_lz_join, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
                        A.pe, A.lzMasks, A.lzState);
     hipLaunchKernelGGL(k_dict_lz_fix, dim3(nb), dim3(64), 0, s, A.dBlocks, A.mlen, A.pe, A.lzMasks, A.lzState);
     hipLaunchKernelGGL(k_dict_lz_clear, dim3((A.nwalk + 3) / 4), dim3(256), 0, s, A.dBlocks, A.walkSegs, A.nwalk, A.mlen,
