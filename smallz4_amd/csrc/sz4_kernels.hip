@@ -984,7 +984,15 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
   )
   if (tid == 0) {
     s_next = 0;
-    s_long = 0;
+    // bounded chains: k_find (pass 2) visits a segment only if it has a long target or an unsearched
+    // (shortcut-interval) one
+    uint32_t sl = 0;
+    if (maxChain < 65535u) {
+      const Interval* iv = ivAll + (uint64_t)S.block * kMaxIv;
+      for (uint32_t j = 0; j < ivCount[S.block]; j++)
+        if (iv[j].lo < S.s1 && iv[j].hi > S.s0) sl = 1;
+    }
+    s_long = sl;
   }
   // kLds: the block's whole window in LDS; otherwise (1) every byte from HBM/L2, so that
   // the LDS holds only the sort and the result tiles and two workgroups share a CU -- the candidates'
@@ -1652,7 +1660,7 @@ __device__ __forceinline__ void find_sorted_body(const uint8_t* __restrict__ in,
       // pass 2 finds a long target's candidates from its slot
       if (active && isLong) rankOut[S.rankOff + rel] = slot;
     }
-    if (unlimited && __ballot(active && isLong) && lane == 0) s_long = 1;
+    if (__ballot(active && isLong) && lane == 0) s_long = 1;
   }
   SZ4_D3(const uint64_t tSearch = __builtin_readcyclecounter();)
   __syncthreads();
@@ -1741,10 +1749,12 @@ __global__ __launch_bounds__(kFindThreads) __attribute__((amdgpu_waves_per_eu(8)
                                                        const uint32_t* __restrict__ ivCount, const uint2* __restrict__ compactAll,
                                                        const uint32_t* __restrict__ rankAll, uint32_t maxChain,
                                                        uint32_t* __restrict__ mlen, uint16_t* __restrict__ mdist,
-                                                       uint64_t matchBase, uint32_t* __restrict__ longFlag)
+                                                       uint64_t matchBase, uint32_t* __restrict__ longFlag,
+                                                       const uint32_t* __restrict__ segLong)
 {
   extern __shared__ __attribute__((aligned(16))) uint32_t win[];
   __shared__ uint32_t s_next;
+  if (!segLong[blockIdx.x]) return;  // pass 1 left nothing here (uniform)
   const Segment S = segs[blockIdx.x];
   const Block B = blocks[S.block];
   const uint32_t tid = threadIdx.x, lane = tid & 63, row = lane >> 4, li = lane & 15;
@@ -6233,7 +6243,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
                            specDist, fix);
     } else
       hipLaunchKernelGGL(k_find<true>, dim3(nsegs), dim3(kFindThreads), find_lds_bytes(), s, in, segs, blocks, iv, ivCount,
-                         compact, rank, maxChain, mlen, mdist, matchBase, longFlag);
+                         compact, rank, maxChain, mlen, mdist, matchBase, longFlag, segLong);
   } else {
     if (pass == 1) {
       // the sort and the text-order result tiles use the same buffer: at least 64 KiB
@@ -6259,7 +6269,7 @@ void launch_find(int pass, const uint8_t* in, const Segment* segs, uint32_t nseg
     }
     else
       hipLaunchKernelGGL(k_find<false>, dim3(nsegs), dim3(kFindThreads), 0, s, in, segs, blocks, iv, ivCount, compact, rank,
-                         maxChain, mlen, mdist, matchBase, longFlag);
+                         maxChain, mlen, mdist, matchBase, longFlag, segLong);
   }
 }
 
