@@ -392,7 +392,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
   uint32_t cursor = first;  // the wavefront's next untaken position (uniform)
   uint32_t i = 0, bestLen = 0, bestDist = 0, steps = 0, hop = 0;
   uint64_t pos = 0, backDist = 0;
-  int64_t room = 0;
+  int64_t room = 0, twAt = -1;  // tw: the target's word at twAt (phase 1's first compare)
+  uint32_t tw = 0;
   bool walking = false, live = false, rmq = false;
   while (true) {
     // lanes without a position take the next ones, in lane order
@@ -422,6 +423,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
           hop = read_slot(P, pe, prevX0, (uint32_t)(pos & kWindow), b, (int64_t)i, B.start, back);
           backDist = 0;
           room = (int64_t)(stop - pos);
+          twAt = -1;
           walking = true;
         }
         if (!walking) {
@@ -474,9 +476,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8), amdgpu_
               }
             }
           }
-          // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3)
+          // phase 1: the bytes between the first one and the first new one, backwards (never bytes 0-3); the
+          // target's first word of it changes only with bestLen: kept in a register (one load per hop fewer)
           int64_t lo = need - 4;
-          while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
+          if (lo > 0) {
+            if (twAt != lo) {
+              tw = gload4(in, pos + lo);
+              twAt = lo;
+            }
+            if (tw == gload4(in, c + lo)) {
+              lo -= 4;
+              while (lo > 0 && gload4(in, pos + lo) == gload4(in, c + lo)) lo -= 4;
+            }
+          }
           if (lo <= 0) {
             // phase 2: forward from the first new byte; 32 bytes per step while they all agree (the loads of
             // a step are independent: one latency per 32 bytes in a long run instead of one per 4)
