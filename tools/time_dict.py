@@ -18,7 +18,9 @@ mb = float(sys.argv[1]) if len(sys.argv) > 1 else 8
 data = synth.enwik8_like(int(mb * 1e6), seed=30)
 dictionary = synth.enwik8_like(65536, seed=31)
 comp = smallz4_amd.Compressor()
-comp.lz4(data[:1 << 20], 65535, dictionary)
+for chain in (65535, 6):  # first calls grow the context's buffers to this input
+    for dic in (b"", dictionary):
+        comp.lz4(data, chain, dic)
 for chain in (65535, 6):
     for dic in (b"", dictionary):
         t = time.perf_counter()
