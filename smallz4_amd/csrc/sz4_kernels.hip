@@ -4830,7 +4830,7 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
     // that could reach one continues in the general loop below
     uint32_t tFast = 0;
     if (cnt == 64u) {
-      if (__ballot(myL > 64u) == 0 && lits + 4u < litBump) {  // every length <= 64
+      if (__ballot(myL > 64u) == 0) {  // every length <= 64
         // Row-transposed batches.  The window is held as lane 16q + j = cost[i0 + 4j + 4 - q] << 6, so the
         // next batch's window is one DPP row shift with the four new costs entering lane 0 of their own
         // row.  The four positions' candidate keys (64 lanes each) are folded into one register by two
@@ -4886,11 +4886,15 @@ __device__ __forceinline__ void dp_spec_body(const Block* __restrict__ blocks,
           w = (uint32_t)__builtin_amdgcn_update_dpp((int)((cp << 6) + rowBias), (int)w, kRowShr + 1, 0xF, 0xF, false);
         };
         uint32_t t = 0;
+        // (a literal run that reaches its next length byte within the first batch starts in the loop below:
+        // the sparse matches of the greedy/lazy levels leave long literal runs)
+        if (lits + 4u < litBump) {
 #pragma unroll
-        for (uint32_t tb = 0; tb < 64; tb += 4) {
-          batch(tb);
-          t = tb + 4u;
-          if (tb + 4u < 64u && lits + 4u >= litBump) break;
+          for (uint32_t tb = 0; tb < 64; tb += 4) {
+            batch(tb);
+            t = tb + 4u;
+            if (tb + 4u < 64u && lits + 4u >= litBump) break;
+          }
         }
         // the rest of the chunk with a literal-length bump reachable: the literal term of the prefix minimum
         // costs one more from the position whose run length reaches litBump on (only the all-literal path
