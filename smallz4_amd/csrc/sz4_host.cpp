@@ -40,11 +40,12 @@ constexpr uint64_t kBatchChunkDefault = 448ull << 20;
 constexpr uint64_t kScratchPerByte = 50;     // device scratch per piece byte, upper bound (36-49 measured)
 constexpr uint64_t kPieceFloor = 16ull << 20;  // smallest batch piece the out-of-memory retry goes down to
 constexpr uint64_t kBlockMax = kBlockMaxDict;  // MaxBlockSize (smallz4.h:124)
-// dictionary rounds before the in-order replay takes the chunk: each round settles at least one more
-// shortcut interval of every block, so a chunk needs at most (intervals per block) + 1 rounds, and a block
-// holds at most one interval per MaxSameLetter + 1 bytes; a chunk that needs more than that (ADVICE r04:
-// the old cap was 4 x kMaxIv = 544 rounds) goes to the replay
-uint32_t dict_round_cap(uint64_t maxBlock) { return (uint32_t)(maxBlock / (kSameLetter + 1)) + 3u; }
+// dictionary rounds before the in-order replay takes the chunk: each round confirms a longer prefix of every
+// block; a wrongly assumed interval may take two rounds (dropped in one, its real start inserted in the
+// next: ADVICE r05), so a chunk needs at most 2 x (intervals per block) + 1 rounds, and a block holds at
+// most one interval per MaxSameLetter + 1 bytes; a chunk that needs more than that (the old
+// cap was 4 x kMaxIv = 544 rounds) goes to the replay
+uint32_t dict_round_cap(uint64_t maxBlock) { return 2u * (uint32_t)(maxBlock / (kSameLetter + 1)) + 3u; }
 
 uint64_t token_capacity(uint64_t n) { return n / 2 + 4; }
 
