@@ -4550,11 +4550,23 @@ __global__ __launch_bounds__(64 * kWalkWaves) void k_lazy_clear(const Block* __r
   w.iv = ivAll + (uint64_t)ws.x * kMaxIv;
   w.niv = ivCount[ws.x];
   w.bstart = B.start;
-  for (uint32_t x0 = a; x0 <= hi; x0 += 64) {
-    const uint32_t x = x0 + lane;
-    const uint64_t inIv = w.niv ? w.ivmask(x0) : 0ull;
-    if (x <= hi && L[x] >= (uint32_t)kMinMatch && !((bw[(x - a) >> 5] >> ((x - a) & 31)) & 1u) && !((inIv >> lane) & 1ull))
-      L[x] = 0;
+  // eight windows' lengths loaded together (unconditional, clamped index), then cleared
+  for (uint32_t x00 = a; x00 <= hi; x00 += 512) {
+    uint32_t lv[8];
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t x = x00 + 64u * u + lane;
+      lv[u] = L[x <= hi ? x : hi];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < 8; u++) {
+      const uint32_t x0 = x00 + 64u * u;
+      if (x0 > hi) break;
+      const uint32_t x = x0 + lane;
+      const uint64_t inIv = w.niv ? w.ivmask(x0) : 0ull;
+      if (x <= hi && lv[u] >= (uint32_t)kMinMatch && !((bw[(x - a) >> 5] >> ((x - a) & 31)) & 1u) && !((inIv >> lane) & 1ull))
+        L[x] = 0;
+    }
   }
 }
 
